@@ -1,0 +1,320 @@
+// hpdct_api.cpp -- the extern "C" boundary (include/hpdct.h): validation,
+// library-owned quantisation table, dispatch to the gfx950 kernels.
+// No torch types, no CPU fallback: every compute entry point launches a HIP
+// kernel or returns an error.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <mutex>
+#include <string>
+
+#include "hpdct.h"
+#include "hpdct_kernels.h"
+
+#define HPDCT_VERSION_STRING "hpdct 0.1.0 (gfx950)"
+
+namespace {
+
+using hpdct::Mat64;
+using hpdct::TileGrid;
+
+// JPEG luminance table and the HpApprDCT matrix (main_newAppr.cu:60-81),
+// host copies; the device copies are compile-time constants in hpdct_tile.hpp.
+constexpr float kDefaultQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                                 14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                                 18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                                 49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+#define TA ((float)0.35355339)
+#define TH ((float)0.5)
+#define TB ((float)0.4472136)
+#define TC ((float)0.2236068)
+#define TD ((float)0.70710678)
+constexpr float kDefaultT[64] = {TA, TA,  TA,  TA,  TA,  TA,  TA,  TA,  TH, TH,  0,   0,   0,   0,   -TH, -TH,
+                                 TB, TC,  -TC, -TB, -TB, -TC, TC,  TB,  0,  0,   -TD, 0,   0,   TD,  0,   0,
+                                 TA, -TA, -TA, TA,  TA,  -TA, -TA, TA,  TH, -TH, 0,   0,   0,   0,   TH,  -TH,
+                                 TC, -TB, TB,  -TC, -TC, TB,  -TB, TC,  0,  0,   0,   -TD, TD,  0,   0,   0};
+#undef TA
+#undef TH
+#undef TB
+#undef TC
+#undef TD
+
+std::mutex g_q_mutex;
+Mat64 g_q = [] {
+    Mat64 m;
+    memcpy(m.v, kDefaultQ, sizeof(m.v));
+    return m;
+}();
+
+thread_local std::string g_last_error;
+
+hpdct_status fail(hpdct_status st, const std::string& msg) {
+    g_last_error = msg;
+    return st;
+}
+
+hpdct_status device_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return HPDCT_SUCCESS;
+    return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+Mat64 current_q() {
+    std::lock_guard<std::mutex> lk(g_q_mutex);
+    return g_q;
+}
+
+// max |q| the forward quantiser can produce for uint8 input with the built-in T:
+// |C[v][u]| <= 128 * ||T_v||_1 * ||T_u||_1 (plus fp rounding), q = round(C/Q).
+bool int8_safe(const Mat64& q) {
+    double n1[8];
+    for (int r = 0; r < 8; ++r) {
+        n1[r] = 0.0;
+        for (int i = 0; i < 8; ++i) n1[r] += std::fabs((double)kDefaultT[r * 8 + i]);
+    }
+    for (int v = 0; v < 8; ++v)
+        for (int u = 0; u < 8; ++u) {
+            const double cmax = 128.0 * n1[v] * n1[u] * (1.0 + 1e-5);
+            if (std::floor(cmax / std::fabs((double)q.v[v * 8 + u]) + 0.5) > 127.0) return false;
+        }
+    return true;
+}
+
+hpdct_status make_grid(int64_t height, int64_t width, TileGrid& g) {
+    if (height <= 0 || width <= 0 || (height % 8) != 0 || (width % 8) != 0)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "height and width must be positive multiples of 8 (got " +
+                                                   std::to_string(height) + "x" + std::to_string(width) + ")");
+    const int64_t tiles = (height / 8) * (width / 8);
+    if (tiles >= (int64_t(1) << 32) || (width / 8) >= (int64_t(1) << 32))
+        return fail(HPDCT_ERROR_INVALID_VALUE, "image too large: tile count must be < 2^32");
+    g.ntiles = static_cast<uint32_t>(tiles);
+    g.tiles_x = static_cast<uint32_t>(width / 8);
+    g.width = static_cast<uint64_t>(width);
+    return HPDCT_SUCCESS;
+}
+
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+uintptr_t row_align(hpdct_dtype t) { return t == HPDCT_F32 ? 16 : 8; }
+size_t elem_size(hpdct_dtype t) { return t == HPDCT_F32 ? 4 : 1; }
+
+}  // namespace
+
+extern "C" {
+
+const char* hpdct_version(void) { return HPDCT_VERSION_STRING; }
+
+const char* hpdct_status_string(hpdct_status s) {
+    switch (s) {
+        case HPDCT_SUCCESS: return "success";
+        case HPDCT_ERROR_INVALID_VALUE: return "invalid value";
+        case HPDCT_ERROR_UNSUPPORTED: return "unsupported dtype/flag combination";
+        case HPDCT_ERROR_RANGE: return "quantised values can overflow int8 with this table";
+        case HPDCT_ERROR_DEVICE: return "HIP runtime error";
+    }
+    return "unknown status";
+}
+
+const char* hpdct_last_error_string(void) { return g_last_error.c_str(); }
+
+void hpdct_default_quant_table(float* q64) {
+    if (q64) memcpy(q64, kDefaultQ, sizeof(kDefaultQ));
+}
+void hpdct_default_transform(float* t64) {
+    if (t64) memcpy(t64, kDefaultT, sizeof(kDefaultT));
+}
+
+hpdct_status hpdct_set_quant_table(const float* q64) {
+    Mat64 m;
+    if (!q64) {
+        memcpy(m.v, kDefaultQ, sizeof(m.v));
+    } else {
+        for (int i = 0; i < 64; ++i)
+            if (!std::isfinite(q64[i]) || q64[i] == 0.0f)
+                return fail(HPDCT_ERROR_INVALID_VALUE, "quant table entries must be finite and non-zero");
+        memcpy(m.v, q64, sizeof(m.v));
+    }
+    std::lock_guard<std::mutex> lk(g_q_mutex);
+    g_q = m;
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_get_quant_table(float* q64) {
+    if (!q64) return fail(HPDCT_ERROR_INVALID_VALUE, "null output pointer");
+    const Mat64 m = current_q();
+    memcpy(q64, m.v, sizeof(m.v));
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coef, hpdct_dtype out_type,
+                           int64_t height, int64_t width, const float* d_transform, unsigned flags, void* stream) {
+    TileGrid g;
+    if (hpdct_status st = make_grid(height, width, g)) return st;
+    if (!d_image || !d_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "null image or coefficient pointer");
+    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_WRITEBACK_SHIFT | HPDCT_FLAG_NO_SHIFT))
+        return fail(HPDCT_ERROR_UNSUPPORTED, "unknown flag bits");
+    if (in_type != HPDCT_U8 && in_type != HPDCT_F32)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "forward input must be HPDCT_U8 or HPDCT_F32");
+    if (out_type != HPDCT_F32 && out_type != HPDCT_I8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "forward output must be HPDCT_F32 or HPDCT_I8");
+    const bool quant = !(flags & HPDCT_FLAG_NO_QUANT);
+    const bool wb = (flags & HPDCT_FLAG_WRITEBACK_SHIFT) != 0;
+    const float shift = (flags & HPDCT_FLAG_NO_SHIFT) ? 0.0f : 128.0f;
+    if (wb && in_type != HPDCT_F32)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "HPDCT_FLAG_WRITEBACK_SHIFT needs an fp32 input");
+    if (out_type == HPDCT_I8) {
+        if (!quant) return fail(HPDCT_ERROR_UNSUPPORTED, "int8 output needs quantisation");
+        if (in_type != HPDCT_U8 || d_transform || shift != 128.0f)
+            return fail(HPDCT_ERROR_UNSUPPORTED, "int8 output needs uint8 input, the built-in T and the level shift");
+    }
+    if (!aligned(d_image, row_align(in_type)) || !aligned(d_coef, row_align(out_type)))
+        return fail(HPDCT_ERROR_INVALID_VALUE, "device pointers must be 16-byte (fp32) / 8-byte (8-bit) aligned");
+    const size_t in_bytes = static_cast<size_t>(height) * width * elem_size(in_type);
+    const char* ib = static_cast<const char*>(d_image);
+    const char* ob = static_cast<const char*>(d_coef);
+    const size_t out_bytes = static_cast<size_t>(height) * width * elem_size(out_type);
+    if (ib < ob + out_bytes && ob < ib + in_bytes)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "image and coefficient buffers overlap");
+    const Mat64 q = current_q();
+    if (out_type == HPDCT_I8 && !int8_safe(q))
+        return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
+
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool bt = d_transform == nullptr;
+    hipError_t e = hipSuccess;
+    using namespace hpdct;
+#define FWD(TI, TO, QN, WB)                                                                                        \
+    e = bt ? launch_fdct<TI, TO, QN, true, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),         \
+                                               static_cast<float*>(const_cast<void*>(d_image)), g, d_transform, q, \
+                                               shift, s)                                                           \
+           : launch_fdct<TI, TO, QN, false, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),        \
+                                                static_cast<float*>(const_cast<void*>(d_image)), g, d_transform,   \
+                                                q, shift, s)
+    if (in_type == HPDCT_U8) {
+        if (out_type == HPDCT_I8) {
+            FWD(uint8_t, int8_t, true, false);
+        } else if (quant) {
+            FWD(uint8_t, float, true, false);
+        } else {
+            FWD(uint8_t, float, false, false);
+        }
+    } else {
+        if (quant && wb) {
+            FWD(float, float, true, true);
+        } else if (quant) {
+            FWD(float, float, true, false);
+        } else if (wb) {
+            FWD(float, float, false, true);
+        } else {
+            FWD(float, float, false, false);
+        }
+    }
+#undef FWD
+    return device_status(e, "forward kernel launch");
+}
+
+hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_image, hpdct_dtype out_type,
+                           int64_t height, int64_t width, const float* d_transform, unsigned flags, void* stream) {
+    TileGrid g;
+    if (hpdct_status st = make_grid(height, width, g)) return st;
+    if (!d_image || !d_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "null image or coefficient pointer");
+    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_NO_SHIFT))
+        return fail(HPDCT_ERROR_UNSUPPORTED, "unknown or forward-only flag bits");
+    if (in_type != HPDCT_F32 && in_type != HPDCT_I8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "inverse input must be HPDCT_F32 or HPDCT_I8");
+    if (out_type != HPDCT_F32 && out_type != HPDCT_U8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "inverse output must be HPDCT_F32 or HPDCT_U8");
+    if (!aligned(d_image, row_align(out_type)) || !aligned(d_coef, row_align(in_type)))
+        return fail(HPDCT_ERROR_INVALID_VALUE, "device pointers must be 16-byte (fp32) / 8-byte (8-bit) aligned");
+    const size_t in_bytes = static_cast<size_t>(height) * width * elem_size(in_type);
+    const size_t out_bytes = static_cast<size_t>(height) * width * elem_size(out_type);
+    const char* ib = static_cast<const char*>(d_coef);
+    const char* ob = static_cast<const char*>(d_image);
+    if (ib < ob + out_bytes && ob < ib + in_bytes)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "coefficient and image buffers overlap");
+    const bool deq = !(flags & HPDCT_FLAG_NO_QUANT);
+    const float shift = (flags & HPDCT_FLAG_NO_SHIFT) ? 0.0f : 128.0f;
+    const Mat64 q = current_q();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool bt = d_transform == nullptr;
+    hipError_t e = hipSuccess;
+    using namespace hpdct;
+#define INV(TI, TO, DQ)                                                                                           \
+    e = bt ? launch_idct<TI, TO, DQ, true>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), g,         \
+                                           d_transform, q, shift, s)                                             \
+           : launch_idct<TI, TO, DQ, false>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), g,        \
+                                            d_transform, q, shift, s)
+#define INV_Q(TI, TO)          \
+    if (deq) {                 \
+        INV(TI, TO, true);     \
+    } else {                   \
+        INV(TI, TO, false);    \
+    }
+    if (in_type == HPDCT_F32) {
+        if (out_type == HPDCT_F32) {
+            INV_Q(float, float)
+        } else {
+            INV_Q(float, uint8_t)
+        }
+    } else {
+        if (out_type == HPDCT_F32) {
+            INV_Q(int8_t, float)
+        } else {
+            INV_Q(int8_t, uint8_t)
+        }
+    }
+#undef INV_Q
+#undef INV
+    return device_status(e, "inverse kernel launch");
+}
+
+hpdct_status hpdct_forward_u8_f32(const uint8_t* d_image, float* d_coef, int64_t height, int64_t width,
+                                  void* stream) {
+    return hpdct_forward(d_image, HPDCT_U8, d_coef, HPDCT_F32, height, width, nullptr, 0u, stream);
+}
+hpdct_status hpdct_forward_u8_i8(const uint8_t* d_image, int8_t* d_coef, int64_t height, int64_t width,
+                                 void* stream) {
+    return hpdct_forward(d_image, HPDCT_U8, d_coef, HPDCT_I8, height, width, nullptr, 0u, stream);
+}
+hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t height, int64_t width,
+                                   void* stream) {
+    return hpdct_inverse(d_coef, HPDCT_F32, d_image, HPDCT_F32, height, width, nullptr, 0u, stream);
+}
+
+hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_t first_index, void* stream) {
+    if (!d_out || n < 0 || first_index < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "bad fill arguments");
+    if (!aligned(d_out, 16)) return fail(HPDCT_ERROR_INVALID_VALUE, "fill target must be 16-byte aligned");
+    if (n == 0) return HPDCT_SUCCESS;
+    return device_status(hpdct::launch_fill_hash(d_out, static_cast<uint64_t>(n), seed,
+                                                 static_cast<uint64_t>(first_index), static_cast<hipStream_t>(stream)),
+                         "fill kernel launch");
+}
+
+// glibc rand() after srand(seed) (benchmark_newAppr.cu:46-51), via the
+// reentrant random_r family so the caller's rand() state is untouched.
+void hpdct_fill_rand_u8(uint8_t* h_out, int64_t n, uint32_t seed) {
+    struct random_data rd;
+    char statebuf[128];
+    memset(&rd, 0, sizeof(rd));
+    initstate_r(seed, statebuf, sizeof(statebuf), &rd);
+    srandom_r(seed, &rd);
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t r;
+        random_r(&rd, &r);
+        h_out[i] = static_cast<uint8_t>(r % 256);
+    }
+}
+
+// convertToFloat (utils.cu:10-15)
+void hpdct_u8_to_f32(const uint8_t* h_in, float* h_out, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) h_out[i] = static_cast<float>(h_in[i]);
+}
+// convertToUnsignedChar (utils.cu:18-24): clamp then truncate
+void hpdct_f32_to_u8(const float* h_in, uint8_t* h_out, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) h_out[i] = static_cast<uint8_t>(fminf(fmaxf(h_in[i], 0.0f), 255.0f));
+}
+
+}  // extern "C"

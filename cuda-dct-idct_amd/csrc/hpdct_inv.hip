@@ -1,0 +1,17 @@
+// hpdct_inv.hip -- inverse kernels.  Kernels: hpdct_kernels_impl.hpp.
+#include "hpdct_kernels_impl.hpp"
+
+namespace hpdct {
+#define HPDCT_INV(TI, TO, DQ, BT)                                                                                  \
+    template hipError_t launch_idct<TI, TO, DQ, BT>(const TI*, TO*, const TileGrid&, const float*, const Mat64&,  \
+                                                    float, hipStream_t);
+#define HPDCT_INV_T(TI, TO, DQ) HPDCT_INV(TI, TO, DQ, true) HPDCT_INV(TI, TO, DQ, false)
+HPDCT_INV_T(float, float, true)
+HPDCT_INV_T(float, float, false)
+HPDCT_INV_T(float, uint8_t, true)
+HPDCT_INV_T(float, uint8_t, false)
+HPDCT_INV_T(int8_t, float, true)
+HPDCT_INV_T(int8_t, float, false)
+HPDCT_INV_T(int8_t, uint8_t, true)
+HPDCT_INV_T(int8_t, uint8_t, false)
+}  // namespace hpdct

@@ -1,0 +1,34 @@
+// hpdct_kernels.h -- host-visible declarations of the gfx950 kernels
+// (launchers are explicit template instantiations in hpdct_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hpdct {
+
+constexpr uint32_t kBlockThreads = 256;  // 4 wave64 per workgroup
+
+// 64 floats passed by value as a kernel argument (lands in SGPRs)
+struct Mat64 {
+    float v[64];
+};
+
+// Tile geometry of one launch: ntiles = (height/8) * (width/8) < 2^32.
+struct TileGrid {
+    uint32_t ntiles;
+    uint32_t tiles_x;
+    uint64_t width;  // elements per image row
+};
+
+template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t launch_fdct(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
+                       const Mat64& q, float shift, hipStream_t s);
+
+template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
+hipError_t launch_idct(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q, float shift,
+                       hipStream_t s);
+
+hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
+
+}  // namespace hpdct

@@ -1,0 +1,160 @@
+// hpdct_tile.hpp -- device-side building blocks of the 8x8 block DCT/IDCT
+// (HpApprDCT arithmetic) for CDNA4 / gfx950.
+//
+// Arithmetic contract (must match the reference bit for bit; see
+// oracle/hpdct_oracle.c and DESIGN.md "Arithmetic contract"):
+//   forward  (main_newAppr.cu:177-211, utils_kernels.cu:8-18,34-44)
+//     X' = X - 128                                   fp32 subtract
+//     P[v][x] = fma chain over i=0..7 of T[v][i]*X'[i][x], from +0
+//     C[v][u] = fma chain over i=0..7 of P[v][i]*T[u][i], from +0
+//     q = roundf(C / Q[v][u])                         IEEE division, half away
+//   inverse  (utils_kernels.cu:47-57, main_newAppr.cu:220-250, utils_kernels.cu:21-31)
+//     D = q * Q[v][u]
+//     P[v][x] = fma chain over i of T[i][v]*D[i][x]
+//     R[v][u] = fma chain over i of P[v][i]*T[i][u];  out = R + 128
+// The whole library is compiled with -ffp-contract=off: every fused
+// multiply-add is an explicit __builtin_fmaf, nothing else may fuse.
+//
+// Zero terms of the built-in T are skipped only where the operand is known
+// finite (uint8 pixels, int8 coefficients): a chain that starts at +0 never
+// holds -0 under round-to-nearest, so fma(0, x, s) == s for finite x and the
+// skip is bit-exact.  fp32 inputs keep every term (an Inf/NaN input must
+// poison the same outputs as in the reference).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "hpdct_kernels.h"
+
+namespace hpdct {
+
+// ---------------------------------------------------------------------------
+// Tables.  The reference stores double literals into a float array
+// (main_newAppr.cu:73-81), so each entry is (float)(double)literal.
+// ---------------------------------------------------------------------------
+#define HPDCT_TA ((float)0.35355339)
+#define HPDCT_TH ((float)0.5)
+#define HPDCT_TB ((float)0.4472136)
+#define HPDCT_TC ((float)0.2236068)
+#define HPDCT_TD ((float)0.70710678)
+inline constexpr Mat64 kBuiltinT = {{
+    HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,
+    HPDCT_TH,  HPDCT_TH,  0.0f,      0.0f,      0.0f,      0.0f,      -HPDCT_TH, -HPDCT_TH,
+    HPDCT_TB,  HPDCT_TC,  -HPDCT_TC, -HPDCT_TB, -HPDCT_TB, -HPDCT_TC, HPDCT_TC,  HPDCT_TB,
+    0.0f,      0.0f,      -HPDCT_TD, 0.0f,      0.0f,      HPDCT_TD,  0.0f,      0.0f,
+    HPDCT_TA,  -HPDCT_TA, -HPDCT_TA, HPDCT_TA,  HPDCT_TA,  -HPDCT_TA, -HPDCT_TA, HPDCT_TA,
+    HPDCT_TH,  -HPDCT_TH, 0.0f,      0.0f,      0.0f,      0.0f,      HPDCT_TH,  -HPDCT_TH,
+    HPDCT_TC,  -HPDCT_TB, HPDCT_TB,  -HPDCT_TC, -HPDCT_TC, HPDCT_TB,  -HPDCT_TB, HPDCT_TC,
+    0.0f,      0.0f,      0.0f,      -HPDCT_TD, HPDCT_TD,  0.0f,      0.0f,      0.0f}};
+#undef HPDCT_TA
+#undef HPDCT_TH
+#undef HPDCT_TB
+#undef HPDCT_TC
+#undef HPDCT_TD
+
+// JPEG luminance table (main_newAppr.cu:60-68)
+inline constexpr Mat64 kDefaultQ = {{16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                                     14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                                     18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                                     49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99}};
+
+// ---------------------------------------------------------------------------
+// Compile-time loop: f(integral_constant<int, I>) for I in [0, N).
+// Every tile index below is a template constant, so table lookups and the
+// zero-term skips fold away at compile time.
+// ---------------------------------------------------------------------------
+template <typename F, int... I>
+__device__ __forceinline__ void unroll_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void unroll(F&& f) {
+    unroll_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------------------
+// Transform source: the built-in matrix (immediates, optional zero skipping)
+// or a caller-provided device matrix (64 wave-uniform scalar loads -> SGPRs).
+// ---------------------------------------------------------------------------
+template <bool kBuiltin, bool kSkipZero>
+struct TSource {
+    float t[kBuiltin ? 1 : 64];
+
+    __device__ __forceinline__ explicit TSource(const float* __restrict__ dev) {
+        if constexpr (!kBuiltin) {
+            unroll<64>([&](auto i) { t[i] = dev[i]; });
+        } else {
+            (void)dev;
+        }
+    }
+    // s + T[IDX] * a, one rounding (the reference's contracted `sums += a*b`)
+    template <int IDX>
+    __device__ __forceinline__ float mac(float a, float s) const {
+        if constexpr (kBuiltin) {
+            constexpr float c = kBuiltinT.v[IDX];
+            if constexpr (kSkipZero && c == 0.0f) {
+                return s;
+            } else {
+                return __builtin_fmaf(c, a, s);
+            }
+        } else {
+            return __builtin_fmaf(t[IDX], a, s);
+        }
+    }
+};
+
+// Forward tile transform on registers: x[i][j] level-shifted pixels,
+// returns P via the column pass, then calls emit(v, c[8]) for each output row
+// (so each row can be quantised and stored while the next is computed).
+template <typename TS, typename Emit>
+__device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& emit) {
+    float p[8][8];
+    // P = T . X   (main_newAppr.cu:193-197): P[v][col] = sum_i T[v][i] X[i][col]
+    unroll<8>([&](auto col) {
+        unroll<8>([&](auto v) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<v * 8 + i>(x[i][col], s); });
+            p[v][col] = s;
+        });
+    });
+    // C = P . T^T (main_newAppr.cu:206-209): C[v][u] = sum_i P[v][i] T[u][i]
+    unroll<8>([&](auto v) {
+        float c[8];
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(p[v][i], s); });
+            c[u] = s;
+        });
+        emit(v, c);
+    });
+}
+
+// Inverse tile transform: d[i][j] dequantised coefficients.
+template <typename TS, typename Emit>
+__device__ __forceinline__ void idct_tile(const TS& T, float (&d)[8][8], Emit&& emit) {
+    float p[8][8];
+    // P = T^T . D (main_newAppr.cu:236-239): P[v][col] = sum_i T[i][v] D[i][col]
+    unroll<8>([&](auto col) {
+        unroll<8>([&](auto v) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<i * 8 + v>(d[i][col], s); });
+            p[v][col] = s;
+        });
+    });
+    // R = P . T (main_newAppr.cu:246-248): R[v][u] = sum_i P[v][i] T[i][u]
+    unroll<8>([&](auto v) {
+        float r[8];
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<i * 8 + u>(p[v][i], s); });
+            r[u] = s;
+        });
+        emit(v, r);
+    });
+}
+
+}  // namespace hpdct

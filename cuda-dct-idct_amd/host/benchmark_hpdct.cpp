@@ -1,0 +1,62 @@
+// benchmark_hpdct.cpp -- HIP-native counterpart of the reference's
+// Benchmark_code/benchmark_newAppr.cu (main, :33-119): same CLI
+// (`benchmark_hpdct <width/height>`), same synthetic input (srand(42),
+// rand()%256 stored as float, :44-51), same Q/T tables, same call sequence
+// (H2D -> dct_all_blocks_cuda -> D2H -> idct_all_blocks_cuda -> D2H) and the
+// same stdout lines "DCT (W,H): x ms" / "IDCT (W,H): x ms", printed by the
+// library's compat entry points.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "hpdct_compat.h"
+
+#define CHECK_HIP(call)                                               \
+    {                                                                 \
+        hipError_t err = call;                                        \
+        if (err != hipSuccess) {                                      \
+            printf("%s : %d", hipGetErrorString(err), __LINE__);      \
+            exit(EXIT_FAILURE);                                       \
+        }                                                             \
+    }
+
+int main(int argc, char* argv[]) {
+    if (argc != 2) {
+        printf("Use: %s <width/height>\n", argv[0]);
+        return 1;
+    }
+    const size_t n = strtoul(argv[1], NULL, 10);
+    const size_t width = n, height = n;
+    const size_t px = width * height;
+
+    float* image = (float*)malloc(px * sizeof(float));
+    srand(42);
+    for (size_t i = 0; i < px; ++i) image[i] = (float)(rand() % 256);
+
+    float transform[64];
+    hpdct_default_transform(transform);  // the T of benchmark_newAppr.cu:67-75
+    // Q: the library's default table is the one of benchmark_newAppr.cu:54-62
+
+    float* result = (float*)malloc(px * sizeof(float));
+    float *d_A, *d_B, *d_C, *d_E;
+    CHECK_HIP(hipMalloc(&d_A, px * sizeof(float)));
+    CHECK_HIP(hipMalloc(&d_B, 64 * sizeof(float)));
+    CHECK_HIP(hipMalloc(&d_C, px * sizeof(float)));
+    CHECK_HIP(hipMemcpy(d_A, image, px * sizeof(float), hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(d_B, transform, 64 * sizeof(float), hipMemcpyHostToDevice));
+
+    dct_all_blocks_cuda(d_A, (int)height, (int)width, d_B, d_C);
+    CHECK_HIP(hipMemcpy(result, d_C, px * sizeof(float), hipMemcpyDeviceToHost));
+
+    CHECK_HIP(hipMalloc(&d_E, px * sizeof(float)));
+    idct_all_blocks_cuda(d_C, (int)height, (int)width, d_B, d_E);
+    CHECK_HIP(hipMemcpy(result, d_E, px * sizeof(float), hipMemcpyDeviceToHost));
+
+    CHECK_HIP(hipFree(d_A));
+    CHECK_HIP(hipFree(d_B));
+    CHECK_HIP(hipFree(d_C));
+    CHECK_HIP(hipFree(d_E));
+    free(result);
+    free(image);
+    return 0;
+}

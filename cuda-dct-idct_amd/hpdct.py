@@ -1,0 +1,296 @@
+"""hpdct -- Python host-side mirror of the reference's DCT/IDCT call surface,
+bound to the gfx950 library ``lib/libhpdct.so`` through its C-ABI
+(``include/hpdct.h``) with ctypes.
+
+PyTorch only supplies device memory and streams here: tensors are passed to
+the library as raw device pointers and the kernels run on torch's current HIP
+stream (or the one given).  There is no CPU or PyTorch fallback: if the
+shared library is missing, every entry point raises ``HpdctLibraryError``.
+
+Reference names mirrored (file:line into GerryDps/CUDA-DCT-IDCT):
+  dct_all_blocks_cuda(image, h, w, T, result)   main_newAppr.cu:252-291
+  idct_all_blocks_cuda(coef, h, w, T, result)   main_newAppr.cu:293-332
+  set_quant_table(q)      cudaMemcpyToSymbol(const_quant_matrix, ...) :19,70
+  convert_to_float / convert_to_unsigned_char   utils.cu:10-24
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HPDCT_LIB", os.path.join(_HERE, "lib", "libhpdct.so"))
+
+# include/hpdct.h
+U8, I8, F32 = 0, 1, 2
+FLAG_NO_QUANT = 0x1
+FLAG_WRITEBACK_SHIFT = 0x2
+FLAG_NO_SHIFT = 0x4
+
+STATUS = {
+    0: "HPDCT_SUCCESS",
+    1: "HPDCT_ERROR_INVALID_VALUE",
+    2: "HPDCT_ERROR_UNSUPPORTED",
+    3: "HPDCT_ERROR_RANGE",
+    4: "HPDCT_ERROR_DEVICE",
+}
+
+# every symbol include/hpdct.h and include/hpdct_compat.h declare
+C_SYMBOLS = [
+    "hpdct_version", "hpdct_status_string", "hpdct_last_error_string",
+    "hpdct_default_quant_table", "hpdct_default_transform",
+    "hpdct_set_quant_table", "hpdct_get_quant_table",
+    "hpdct_forward", "hpdct_inverse",
+    "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
+    "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
+]
+COMPAT_SYMBOLS = {
+    "dct_all_blocks_cuda": "_Z19dct_all_blocks_cudaPfiiPKfS_",
+    "idct_all_blocks_cuda": "_Z20idct_all_blocks_cudaPKfiiS0_Pf",
+}
+
+
+class HpdctLibraryError(RuntimeError):
+    """libhpdct.so is missing or failed to load (no fallback exists)."""
+
+
+class HpdctError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS.get(status, status)}: {message}")
+        self.status = status
+
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and return the native library; raise loudly if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise HpdctLibraryError(
+            f"{p} not found: build it with `make -C cuda-dct-idct_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError as e:  # pragma: no cover - depends on the loader
+        raise HpdctLibraryError(f"cannot load {p}: {e}") from e
+    vp, i64, u32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32
+    lib.hpdct_version.restype = ctypes.c_char_p
+    lib.hpdct_status_string.restype = ctypes.c_char_p
+    lib.hpdct_status_string.argtypes = [ctypes.c_int]
+    lib.hpdct_last_error_string.restype = ctypes.c_char_p
+    for f in (lib.hpdct_default_quant_table, lib.hpdct_default_transform):
+        f.argtypes = [vp]
+        f.restype = None
+    lib.hpdct_set_quant_table.argtypes = [vp]
+    lib.hpdct_get_quant_table.argtypes = [vp]
+    for f in (lib.hpdct_forward, lib.hpdct_inverse):
+        f.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, i64, i64, vp, ctypes.c_uint, vp]
+        f.restype = ctypes.c_int
+    for f in (lib.hpdct_forward_u8_f32, lib.hpdct_forward_u8_i8, lib.hpdct_inverse_f32_f32):
+        f.argtypes = [vp, vp, i64, i64, vp]
+        f.restype = ctypes.c_int
+    lib.hpdct_fill_hash_u8.argtypes = [vp, i64, ctypes.c_uint64, i64, vp]
+    lib.hpdct_fill_hash_u8.restype = ctypes.c_int
+    lib.hpdct_fill_rand_u8.argtypes = [vp, i64, u32]
+    lib.hpdct_fill_rand_u8.restype = None
+    lib.hpdct_u8_to_f32.argtypes = [vp, vp, i64]
+    lib.hpdct_u8_to_f32.restype = None
+    lib.hpdct_f32_to_u8.argtypes = [vp, vp, i64]
+    lib.hpdct_f32_to_u8.restype = None
+    for name, mangled in COMPAT_SYMBOLS.items():
+        f = getattr(lib, mangled)
+        f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+        f.restype = None
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(status: int) -> None:
+    if status != 0:
+        msg = load_library().hpdct_last_error_string().decode(errors="replace")
+        raise HpdctError(status, msg)
+
+
+def version() -> str:
+    return load_library().hpdct_version().decode()
+
+
+# ---------------------------------------------------------------------------
+# tables
+# ---------------------------------------------------------------------------
+def default_quant_table() -> np.ndarray:
+    q = np.empty(64, np.float32)
+    load_library().hpdct_default_quant_table(q.ctypes.data)
+    return q.reshape(8, 8)
+
+
+def default_transform() -> np.ndarray:
+    t = np.empty(64, np.float32)
+    load_library().hpdct_default_transform(t.ctypes.data)
+    return t.reshape(8, 8)
+
+
+def set_quant_table(q) -> None:
+    """Library-owned Q (replaces cudaMemcpyToSymbol(const_quant_matrix, ...)).
+    ``None`` restores the default JPEG luminance table."""
+    lib = load_library()
+    if q is None:
+        _check(lib.hpdct_set_quant_table(None))
+        return
+    a = np.ascontiguousarray(np.asarray(q, dtype=np.float32).reshape(64))
+    _check(lib.hpdct_set_quant_table(a.ctypes.data))
+
+
+def get_quant_table() -> np.ndarray:
+    q = np.empty(64, np.float32)
+    _check(load_library().hpdct_get_quant_table(q.ctypes.data))
+    return q.reshape(8, 8)
+
+
+# ---------------------------------------------------------------------------
+# device entry points (torch tensors in HBM)
+# ---------------------------------------------------------------------------
+def _torch():
+    import torch
+    return torch
+
+
+def _dtype_code(t) -> int:
+    torch = _torch()
+    m = {torch.uint8: U8, torch.int8: I8, torch.float32: F32}
+    if t.dtype not in m:
+        raise HpdctError(2, f"unsupported tensor dtype {t.dtype}")
+    return m[t.dtype]
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _hw(t, height, width):
+    if height is None or width is None:
+        if t.dim() < 2:
+            raise HpdctError(1, "pass height/width for a flat tensor")
+        height = t.numel() // t.shape[-1]
+        width = t.shape[-1]
+    return int(height), int(width)
+
+
+def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, writeback_shift=False,
+            level_shift=True, height=None, width=None, stream=None):
+    """Fused forward pass on the GPU: round((T.(X-128).T^T)/Q) per 8x8 tile.
+
+    image: CUDA tensor, uint8 or float32, (..., H, W) contiguous (a stack of
+    frames is treated as one (F*H) x W image).  Returns the coefficient
+    tensor (float32 by default, int8 on request) in the reference layout."""
+    torch = _torch()
+    if not image.is_cuda or not image.is_contiguous():
+        raise HpdctError(1, "image must be a contiguous CUDA tensor")
+    h, w = _hw(image, height, width)
+    if out is None:
+        out = torch.empty(image.shape, dtype=out_dtype or torch.float32, device=image.device)
+    flags = (0 if quantise else FLAG_NO_QUANT) | (FLAG_WRITEBACK_SHIFT if writeback_shift else 0) | \
+        (0 if level_shift else FLAG_NO_SHIFT)
+    tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
+    _check(load_library().hpdct_forward(ctypes.c_void_p(image.data_ptr()), _dtype_code(image),
+                                        ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
+                                        flags, _stream_ptr(stream)))
+    return out
+
+
+def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, level_shift=True,
+            height=None, width=None, stream=None):
+    """Fused inverse pass: T^T.(q*Q).T + 128 per tile.  out float32 (no clamp,
+    as the reference) or uint8 (clamp + truncate, convertToUnsignedChar)."""
+    torch = _torch()
+    if not coef.is_cuda or not coef.is_contiguous():
+        raise HpdctError(1, "coefficients must be a contiguous CUDA tensor")
+    h, w = _hw(coef, height, width)
+    if out is None:
+        out = torch.empty(coef.shape, dtype=out_dtype or torch.float32, device=coef.device)
+    flags = (0 if dequantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT)
+    tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
+    _check(load_library().hpdct_inverse(ctypes.c_void_p(coef.data_ptr()), _dtype_code(coef),
+                                        ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
+                                        flags, _stream_ptr(stream)))
+    return out
+
+
+def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift=True, stream=None,
+         height=None, width=None):
+    """Pre-resolve every argument of one forward ("fwd") or inverse ("inv")
+    launch and return a zero-argument callable: the per-call host cost is one
+    ctypes call (used by bench.py's timed loop)."""
+    if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()):
+        raise HpdctError(1, "src/dst must be contiguous CUDA tensors")
+    h, w = _hw(src, height, width)
+    lib = load_library()
+    fn = {"fwd": lib.hpdct_forward, "inv": lib.hpdct_inverse}[direction]
+    flags = (0 if quantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT)
+    args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(dst.data_ptr()), _dtype_code(dst),
+            h, w, None if transform is None else ctypes.c_void_p(transform.data_ptr()), flags, _stream_ptr(stream))
+
+    def call():
+        st = fn(*args)
+        if st:
+            _check(st)
+    return call
+
+
+def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):
+    """Device-side synthetic frame: out[i] = splitmix64(seed, first_index+i) & 255."""
+    _check(load_library().hpdct_fill_hash_u8(ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                             ctypes.c_uint64(seed), first_index, _stream_ptr(stream)))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# the reference's own C++ entry points (compat layer, synchronous, prints)
+# ---------------------------------------------------------------------------
+def dct_all_blocks_cuda(image_matrix, img_height: int, img_width: int, transform_matrix, result) -> None:
+    """main_newAppr.cu:252-291 semantics: device fp32 buffers, caller's T,
+    X-128 left in image_matrix, timing line on stdout, exits on error."""
+    f = getattr(load_library(), COMPAT_SYMBOLS["dct_all_blocks_cuda"])
+    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
+      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()))
+
+
+def idct_all_blocks_cuda(image_matrix, img_height: int, img_width: int, transform_matrix, result) -> None:
+    """main_newAppr.cu:293-332 semantics."""
+    f = getattr(load_library(), COMPAT_SYMBOLS["idct_all_blocks_cuda"])
+    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
+      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()))
+
+
+# ---------------------------------------------------------------------------
+# host helpers (no device work)
+# ---------------------------------------------------------------------------
+def fill_rand_u8(n: int, seed: int = 42) -> np.ndarray:
+    """srand(seed); rand() % 256, n values (benchmark_newAppr.cu:46-51)."""
+    a = np.empty(int(n), np.uint8)
+    load_library().hpdct_fill_rand_u8(a.ctypes.data, int(n), ctypes.c_uint32(seed))
+    return a
+
+
+def convert_to_float(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    o = np.empty(a.shape, np.float32)
+    load_library().hpdct_u8_to_f32(a.ctypes.data, o.ctypes.data, a.size)
+    return o
+
+
+def convert_to_unsigned_char(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    o = np.empty(a.shape, np.uint8)
+    load_library().hpdct_f32_to_u8(a.ctypes.data, o.ctypes.data, a.size)
+    return o

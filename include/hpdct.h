@@ -1,0 +1,132 @@
+/*
+ * hpdct.h -- native C-ABI of the MI355X (gfx950) 8x8 block DCT/IDCT +
+ * quantisation path (HpApprDCT arithmetic).  Library: libhpdct.so
+ * (cuda-dct-idct_amd/lib/).
+ *
+ * Every entry point takes plain device pointers, 64-bit sizes and an optional
+ * HIP stream (hipStream_t passed as void*; NULL = the null stream), returns a
+ * status code and never exits the process.  The reference's own C++ entry
+ * points (dct_all_blocks_cuda / idct_all_blocks_cuda, with their
+ * print-and-exit semantics) are in hpdct_compat.h and are implemented on top
+ * of these.
+ *
+ * Reference interface each function replaces (file:line into the reference,
+ * GerryDps/CUDA-DCT-IDCT):
+ *   hpdct_forward          dct_all_blocks_cuda      main_newAppr.cu:252-291
+ *                          (sub_matrix_scalar -> cuda_matrix_dct ->
+ *                          divide_matrices fused into one pass)
+ *   hpdct_inverse          idct_all_blocks_cuda     main_newAppr.cu:293-332
+ *                          (multiply_matrices -> cuda_matrix_idct ->
+ *                          add_matrix_scalar fused into one pass)
+ *   hpdct_set_quant_table  cudaMemcpyToSymbol(const_quant_matrix, ...)
+ *                          main_newAppr.cu:19,70 (Q is library-owned here)
+ *   hpdct_default_*        the Q and T tables of main_newAppr.cu:60-81
+ *   hpdct_fill_rand_u8     not a device op in the reference: the synthetic
+ *   (host)                 input of benchmark_newAppr.cu:46-51
+ *                          (srand(42); rand()%256), restated
+ *   hpdct_u8_from_f32 ... host conversions utils.cu:10-24
+ *
+ * Layout: an image is `height` rows of `width` elements, row-major, densely
+ * packed (row pitch == width elements).  Coefficients are written in the
+ * reference's spatial layout: coefficient (v,u) of tile (by,bx) sits at
+ * [(8*by + v) * width + 8*bx + u].  A batch of F frames of HxW stacked in
+ * memory is the single image (F*H) x W: tiles never cross a frame boundary
+ * when H is a multiple of 8.  height and width must be positive multiples of
+ * 8 (the reference silently produces garbage otherwise; we refuse).
+ */
+#ifndef HPDCT_H
+#define HPDCT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum hpdct_status {
+    HPDCT_SUCCESS = 0,
+    HPDCT_ERROR_INVALID_VALUE = 1, /* NULL pointer, size not a positive multiple of 8, too many tiles */
+    HPDCT_ERROR_UNSUPPORTED = 2,   /* dtype / flag combination not provided */
+    HPDCT_ERROR_RANGE = 3,         /* int8 coefficients requested but the quant table can overflow int8 */
+    HPDCT_ERROR_DEVICE = 4         /* a HIP runtime call failed: see hpdct_last_error_string() */
+} hpdct_status;
+
+typedef enum hpdct_dtype {
+    HPDCT_U8 = 0,  /* uint8 pixels (0..255)                                   */
+    HPDCT_I8 = 1,  /* int8 quantised coefficients (wire format, |q| <= 127)   */
+    HPDCT_F32 = 2  /* fp32 pixels or coefficients (the reference's only type) */
+} hpdct_dtype;
+
+/* Flags for hpdct_forward / hpdct_inverse. */
+#define HPDCT_FLAG_NO_QUANT 0x1u       /* forward: skip /Q+round; inverse: skip xQ (raw coefficients) */
+#define HPDCT_FLAG_WRITEBACK_SHIFT 0x2u /* forward, f32 input only: also store X-128 back into the
+                                           input buffer, as the reference's in-place sub_matrix_scalar
+                                           does (main_newAppr.cu:273) */
+#define HPDCT_FLAG_NO_SHIFT 0x4u       /* skip the -128 / +128 level shift (diagnostics, round trips) */
+
+/* Library / error information. */
+const char* hpdct_version(void);
+const char* hpdct_status_string(hpdct_status status);
+const char* hpdct_last_error_string(void); /* thread-local, last failing call */
+
+/* Built-in tables (main_newAppr.cu:60-68 Q, :73-81 T), copied into caller memory. */
+void hpdct_default_quant_table(float* q64);
+void hpdct_default_transform(float* t64);
+
+/* Library-owned quantisation table used by every subsequent forward/inverse
+ * call (process-wide).  q64: HOST pointer to 64 floats, row-major [v][u];
+ * NULL restores the default JPEG luminance table.  Entries must be finite and
+ * non-zero. */
+hpdct_status hpdct_set_quant_table(const float* q64);
+hpdct_status hpdct_get_quant_table(float* q64);
+
+/* Forward 8x8 block transform.
+ *   d_image    : device, height*width elements of in_type (HPDCT_U8 or HPDCT_F32)
+ *   d_coef     : device, height*width elements of out_type (HPDCT_F32, or
+ *                HPDCT_I8 with quantisation on)
+ *   d_transform: device pointer to 64 floats T[v][i], or NULL for the
+ *                built-in HpApprDCT matrix
+ *   flags      : HPDCT_FLAG_*
+ *   stream     : hipStream_t or NULL
+ * Computes, per tile, q = round((T . (X-128) . T^T) / Q) with the reference's
+ * fp32 fused-multiply-add order and IEEE division.  Asynchronous w.r.t. the
+ * host.  d_image and d_coef must not overlap (except that d_image is written
+ * with X-128 under HPDCT_FLAG_WRITEBACK_SHIFT). */
+hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coef, hpdct_dtype out_type,
+                           int64_t height, int64_t width, const float* d_transform, unsigned flags,
+                           void* stream);
+
+/* Inverse 8x8 block transform.
+ *   d_coef : device, height*width elements of in_type (HPDCT_F32 or HPDCT_I8)
+ *   d_image: device, height*width elements of out_type: HPDCT_F32 (R+128, no
+ *            clamp, as the reference) or HPDCT_U8 (then clamped to [0,255] and
+ *            truncated, as convertToUnsignedChar, utils.cu:18-24)
+ * Computes R = T^T . (q*Q) . T + 128 per tile. */
+hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_image, hpdct_dtype out_type,
+                           int64_t height, int64_t width, const float* d_transform, unsigned flags,
+                           void* stream);
+
+/* Typed shorthands for the common cases (built-in T, library Q). */
+hpdct_status hpdct_forward_u8_f32(const uint8_t* d_image, float* d_coef, int64_t height, int64_t width,
+                                  void* stream);
+hpdct_status hpdct_forward_u8_i8(const uint8_t* d_image, int8_t* d_coef, int64_t height, int64_t width,
+                                 void* stream);
+hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t height, int64_t width,
+                                   void* stream);
+
+/* Synthetic frames generated on the device (BASELINE config C4): pixel
+ * i of the frame = splitmix64(seed, first_index + i) & 255 (the oracle's
+ * oracle_fill_hash_u8 restates it). */
+hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_t first_index, void* stream);
+
+/* Host-side helpers (no device work). */
+void hpdct_fill_rand_u8(uint8_t* h_out, int64_t n, uint32_t seed); /* srand(seed); rand()%256 (glibc TYPE_3) */
+void hpdct_u8_to_f32(const uint8_t* h_in, float* h_out, int64_t n); /* convertToFloat, utils.cu:10-15 */
+void hpdct_f32_to_u8(const float* h_in, uint8_t* h_out, int64_t n); /* convertToUnsignedChar, utils.cu:18-24 */
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* HPDCT_H */

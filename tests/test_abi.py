@@ -1,0 +1,144 @@
+"""CPU-side checks of the C-ABI boundary (no compute calls: there is no GPU here).
+
+- libhpdct.so loads and exports every function include/*.h declares, with
+  the reference's C++ mangled names for the compat entry points;
+- argument validation fails with the documented status before any device
+  work is attempted;
+- the host helpers reproduce the reference's input stream and conversions.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def header_functions():
+    names = set()
+    for fn in os.listdir(INCLUDE):
+        if not fn.endswith(".h"):
+            continue
+        text = open(os.path.join(INCLUDE, fn)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"\b([A-Za-z_]\w*)\s*\([^;{}()]*\)\s*;", text):
+            names.add(m.group(1))
+    return names
+
+
+def exported_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_library_exports_every_declared_symbol(hp):
+    declared = header_functions()
+    assert {"hpdct_forward", "hpdct_inverse", "dct_all_blocks_cuda", "idct_all_blocks_cuda"} <= declared
+    syms = exported_symbols(hp.LIB_PATH)
+    for name in declared:
+        if name in hp.COMPAT_SYMBOLS:
+            assert hp.COMPAT_SYMBOLS[name] in syms, name
+        else:
+            assert name in syms, name
+    assert set(hp.C_SYMBOLS) | set(hp.COMPAT_SYMBOLS) == declared
+
+
+def test_compat_mangling_matches_reference_signatures(tmp_path):
+    # what g++ emits for the reference's own declarations (main_newAppr.cu:23-24)
+    src = tmp_path / "decl.cpp"
+    src.write_text(
+        "void dct_all_blocks_cuda(float* image_matrix, const int img_height, const int img_width,"
+        " const float* transform_matrix, float* result) {}\n"
+        "void idct_all_blocks_cuda(const float* image_matrix, const int img_height, const int img_width,"
+        " const float* transform_matrix, float* result) {}\n")
+    obj = tmp_path / "decl.o"
+    subprocess.run(["g++", "-c", str(src), "-o", str(obj)], check=True)
+    out = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
+    assert "_Z19dct_all_blocks_cudaPfiiPKfS_" in out
+    assert "_Z20idct_all_blocks_cudaPKfiiS0_Pf" in out
+
+
+def test_kernels_are_gfx950_code_objects(hp):
+    data = open(hp.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"_ZN5hpdct11fdct_kernel" in data and b"_ZN5hpdct11idct_kernel" in data
+
+
+def test_version_and_status_strings(hp):
+    assert "gfx950" in hp.version()
+    L = hp.load_library()
+    assert L.hpdct_status_string(0) == b"success"
+    assert L.hpdct_status_string(3).startswith(b"quantised")
+
+
+def test_tables_match_reference(hp, oracle):
+    assert np.array_equal(hp.default_transform().view(np.uint32), oracle.default_transform().view(np.uint32))
+    assert np.array_equal(hp.default_quant_table(), oracle.default_quant())
+
+
+def test_quant_table_state(hp):
+    q = np.arange(1, 65, dtype=np.float32).reshape(8, 8)
+    hp.set_quant_table(q)
+    try:
+        assert np.array_equal(hp.get_quant_table(), q)
+    finally:
+        hp.set_quant_table(None)
+    assert np.array_equal(hp.get_quant_table(), hp.default_quant_table())
+    bad = np.ones(64, np.float32)
+    bad[5] = 0.0
+    with pytest.raises(hp.HpdctError) as e:
+        hp.set_quant_table(bad)
+    assert e.value.status == 1
+    bad[5] = np.nan
+    with pytest.raises(hp.HpdctError):
+        hp.set_quant_table(bad)
+    assert np.array_equal(hp.get_quant_table(), hp.default_quant_table())
+
+
+@pytest.mark.parametrize("h,w", [(0, 8), (8, 0), (12, 8), (8, 20), (-8, 8), (7, 7)])
+def test_bad_shapes_rejected_before_device_work(hp, h, w):
+    L = hp.load_library()
+    dummy = ctypes.c_void_p(256)  # never dereferenced: validation fails first
+    st = L.hpdct_forward(dummy, hp.U8, ctypes.c_void_p(4096), hp.F32, h, w, None, 0, None)
+    assert st == 1
+    assert b"multiples of 8" in L.hpdct_last_error_string()
+    st = L.hpdct_inverse(dummy, hp.F32, ctypes.c_void_p(4096), hp.F32, h, w, None, 0, None)
+    assert st == 1
+
+
+def test_bad_arguments_rejected(hp):
+    L = hp.load_library()
+    a, b = ctypes.c_void_p(1 << 20), ctypes.c_void_p(1 << 30)
+    assert L.hpdct_forward(None, hp.U8, b, hp.F32, 8, 8, None, 0, None) == 1
+    assert L.hpdct_forward(a, hp.I8, b, hp.F32, 8, 8, None, 0, None) == 2  # int8 is not an image type
+    assert L.hpdct_forward(a, hp.U8, b, hp.U8, 8, 8, None, 0, None) == 2
+    assert L.hpdct_forward(a, hp.U8, b, hp.I8, 8, 8, None, hp.FLAG_NO_QUANT, None) == 2
+    assert L.hpdct_forward(a, hp.U8, b, hp.F32, 8, 8, None, hp.FLAG_WRITEBACK_SHIFT, None) == 2
+    assert L.hpdct_forward(a, hp.U8, b, hp.F32, 8, 8, None, 0x80, None) == 2
+    assert L.hpdct_forward(ctypes.c_void_p((1 << 20) + 4), hp.F32, b, hp.F32, 8, 8, None, 0, None) == 1
+    assert L.hpdct_forward(a, hp.F32, ctypes.c_void_p((1 << 20) + 64), hp.F32, 8, 8, None, 0, None) == 1  # overlap
+    assert L.hpdct_inverse(a, hp.U8, b, hp.F32, 8, 8, None, 0, None) == 2
+    assert L.hpdct_inverse(a, hp.F32, b, hp.I8, 8, 8, None, 0, None) == 2
+    assert L.hpdct_inverse(a, hp.F32, b, hp.F32, 8, 8, None, hp.FLAG_WRITEBACK_SHIFT, None) == 2
+    # int8 output refused when the table can overflow int8
+    hp.set_quant_table(np.ones(64, np.float32))
+    try:
+        assert L.hpdct_forward(a, hp.U8, b, hp.I8, 8, 8, None, 0, None) == 3
+    finally:
+        hp.set_quant_table(None)
+
+
+def test_host_rand_matches_glibc(hp, oracle):
+    assert np.array_equal(hp.fill_rand_u8(100000, 42), oracle.rand_u8(100000, 42))
+    assert np.array_equal(hp.fill_rand_u8(5000, 7), oracle.rand_u8(5000, 7))
+
+
+def test_host_conversions_match_reference(hp, oracle):
+    z = np.load(os.path.join(ROOT, "tests", "golden", "ref_utils_convert.npz"))
+    assert np.array_equal(hp.convert_to_float(z["u8_in"]), z["f32_out"])
+    assert np.array_equal(hp.convert_to_unsigned_char(z["f32_in"]), z["u8_out"])

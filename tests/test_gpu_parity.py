@@ -1,0 +1,296 @@
+"""GPU parity: the gfx950 kernels against the CPU oracle, through the C-ABI.
+
+Bar: quantised coefficients and every fp32 plane BIT-EXACT (the oracle
+restates the reference's fp32 FMA chain, IEEE division and roundf), compared
+as uint32 bit patterns (so -0.0 must match too).  NaN outputs compare by
+position (payload bits are not part of the contract).
+"""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    return np.array_equal(np.where(na, 0, a.view(np.uint32)), np.where(nb, 0, b.view(np.uint32)))
+
+
+def mismatches(a, b):
+    return int((np.ascontiguousarray(a, np.float32).view(np.uint32) != np.ascontiguousarray(b, np.float32).view(np.uint32)).sum())
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLD, "golden.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def c1(oracle):
+    return oracle.rand_u8(256 * 256, 42).reshape(256, 256)
+
+
+def to_dev(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def to_host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# --------------------------------------------------------------------- forward
+def test_c1_forward_u8_f32_bitexact(hp, oracle, dev, c1, golden):
+    q = to_host(hp.forward(to_dev(c1, dev)))
+    ref = oracle.fdct(c1)
+    assert mismatches(q, ref) == 0
+    assert sha(q) == golden["configs"]["c1_256"]["q_f32_sha256"]
+
+
+def test_c1_forward_f32_input_bitexact(hp, oracle, dev, c1, golden):
+    img = c1.astype(np.float32)
+    t = to_dev(img, dev)
+    q = to_host(hp.forward(t))
+    assert sha(q) == golden["configs"]["c1_256"]["q_f32_sha256"]
+    assert np.array_equal(to_host(t), img)  # native API does not mutate
+
+
+def test_c1_forward_int8_matches_golden(hp, dev, c1):
+    import torch
+    q = to_host(hp.forward(to_dev(c1, dev), out_dtype=torch.int8))
+    assert np.array_equal(q, np.load(os.path.join(GOLD, "c1_256_seed42_q_i8.npy")))
+
+
+def test_forward_unquantised_bitexact(hp, oracle, dev, c1, golden):
+    c = to_host(hp.forward(to_dev(c1, dev), quantise=False))
+    assert sha(c) == golden["configs"]["c1_256"]["coef_f32_sha256"]
+    c32 = to_host(hp.forward(to_dev(c1.astype(np.float32), dev), quantise=False))
+    assert bits_equal(c32, oracle.fdct(c1, quant=False))
+
+
+def test_forward_no_level_shift(hp, oracle, dev, c1):
+    c = to_host(hp.forward(to_dev(c1, dev), quantise=False, level_shift=False))
+    assert bits_equal(c, oracle.fdct(c1, quant=False, shift=False))
+
+
+def test_runtime_transform_equals_builtin(hp, oracle, dev, c1):
+    # the caller's T (device buffer) takes the dense-FMA kernel; same bits
+    T = to_dev(hp.default_transform(), dev)
+    a = to_host(hp.forward(to_dev(c1, dev), transform=T))
+    b = to_host(hp.forward(to_dev(c1.astype(np.float32), dev), transform=T))
+    ref = oracle.fdct(c1)
+    assert bits_equal(a, ref) and bits_equal(b, ref)
+
+
+def test_custom_transform_and_quant(hp, oracle, dev, c1):
+    rng = np.random.default_rng(5)
+    T = np.linalg.qr(rng.standard_normal((8, 8)))[0].astype(np.float32)
+    Q = rng.integers(1, 120, (8, 8)).astype(np.float32)
+    hp.set_quant_table(Q)
+    try:
+        got = to_host(hp.forward(to_dev(c1, dev), transform=to_dev(T, dev)))
+        got32 = to_host(hp.forward(to_dev(c1.astype(np.float32), dev), transform=to_dev(T, dev)))
+        builtin = to_host(hp.forward(to_dev(c1, dev)))
+    finally:
+        hp.set_quant_table(None)
+    assert bits_equal(got, oracle.fdct(c1, T=T, Q=Q))
+    assert bits_equal(got32, oracle.fdct(c1, T=T, Q=Q))
+    assert bits_equal(builtin, oracle.fdct(c1, Q=Q))
+
+
+@pytest.mark.parametrize("h,w", [(8, 8), (8, 16), (16, 8), (24, 40), (8, 4096), (520, 8), (1000, 1008), (72, 2056)])
+def test_forward_shapes(hp, oracle, dev, h, w):
+    img = np.random.default_rng(h * 7919 + w).integers(0, 256, (h, w), dtype=np.uint8)
+    assert bits_equal(to_host(hp.forward(to_dev(img, dev))), oracle.fdct(img))
+    assert bits_equal(to_host(hp.forward(to_dev(img.astype(np.float32), dev))), oracle.fdct(img))
+
+
+def test_forward_extremes(hp, oracle, dev):
+    t = oracle.default_transform()
+    tiles = []
+    for v in range(8):
+        for u in range(8):
+            s = np.sign(np.outer(t[v], t[u]))
+            tiles.append(np.where(s > 0, 255, 0))
+            tiles.append(np.where(s > 0, 0, 255))
+    tiles += [np.zeros((8, 8)), np.full((8, 8), 255), np.full((8, 8), 128)]
+    img = np.concatenate(tiles, axis=1).astype(np.uint8)  # 8 x (8*131)
+    img = np.ascontiguousarray(img)
+    q = to_host(hp.forward(to_dev(img, dev)))
+    assert bits_equal(q, oracle.fdct(img))
+    assert np.abs(q).max() <= 98
+    import torch
+    q8 = to_host(hp.forward(to_dev(img, dev), out_dtype=torch.int8))
+    assert np.array_equal(q8, oracle.fdct(img).astype(np.int8))
+
+
+def test_forward_nonfinite_fp32_input(hp, oracle, dev):
+    img = np.random.default_rng(1).uniform(-1e3, 1e3, (16, 32)).astype(np.float32)
+    img[1, 2] = np.inf
+    img[9, 20] = np.nan
+    img[12, 5] = -np.inf
+    img[3, 30] = 3.0e38
+    img[5, 17] = 1e-42  # denormal
+    got = to_host(hp.forward(to_dev(img, dev)))
+    assert bits_equal(got, oracle.fdct(img))
+    got = to_host(hp.forward(to_dev(img, dev), quantise=False))
+    assert bits_equal(got, oracle.fdct(img, quant=False))
+
+
+def test_batch_of_frames(hp, oracle, dev):
+    frames = np.random.default_rng(2).integers(0, 256, (3, 64, 128), dtype=np.uint8)
+    got = to_host(hp.forward(to_dev(frames, dev)))
+    for f in range(3):
+        assert bits_equal(got[f], oracle.fdct(frames[f]))
+
+
+def test_tile_independence(hp, dev, c1):
+    a = to_host(hp.forward(to_dev(c1, dev)))
+    img = c1.copy()
+    img[64:72, 128:136] = 255 - img[64:72, 128:136]
+    b = to_host(hp.forward(to_dev(img, dev)))
+    d = a != b
+    d[64:72, 128:136] = False
+    assert not d.any()
+
+
+def test_non_default_stream_and_determinism(hp, dev, c1):
+    import torch
+    s = torch.cuda.Stream()
+    x = to_dev(c1, dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        a = hp.forward(x)
+    s.synchronize()
+    b = hp.forward(x, stream=s)
+    s.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_misaligned_pointer_rejected(hp, dev):
+    import torch
+    buf = torch.zeros(8 * 8 + 1, dtype=torch.float32, device=dev)
+    with pytest.raises(hp.HpdctError) as e:
+        hp.forward(buf[1:].view(8, 8))
+    assert e.value.status == 1
+
+
+# --------------------------------------------------------------------- inverse
+def test_c1_inverse_f32_bitexact(hp, oracle, dev, c1, golden):
+    q = oracle.fdct(c1)
+    r = to_host(hp.inverse(to_dev(q, dev)))
+    assert sha(r) == golden["configs"]["c1_256"]["roundtrip_f32_sha256"]
+    assert bits_equal(r, oracle.idct(q))
+
+
+def test_inverse_outputs_and_inputs(hp, oracle, dev, c1):
+    import torch
+    q = oracle.fdct(c1)
+    ref = oracle.idct(q)
+    ref8 = oracle.to_u8(ref)
+    assert np.array_equal(to_host(hp.inverse(to_dev(q, dev), out_dtype=torch.uint8)), ref8)
+    qi8 = to_dev(q.astype(np.int8), dev)
+    assert bits_equal(to_host(hp.inverse(qi8)), ref)
+    assert np.array_equal(to_host(hp.inverse(qi8, out_dtype=torch.uint8)), ref8)
+
+
+def test_inverse_unquantised_and_runtime_T(hp, oracle, dev, c1):
+    c = oracle.fdct(c1, quant=False)
+    r = to_host(hp.inverse(to_dev(c, dev), dequantise=False))
+    assert bits_equal(r, oracle.idct(c, dequant=False))
+    assert np.abs(r - c1).max() < 1e-4
+    T = to_dev(hp.default_transform(), dev)
+    r2 = to_host(hp.inverse(to_dev(c, dev), dequantise=False, transform=T))
+    assert bits_equal(r2, r)
+    rng = np.random.default_rng(9)
+    Tc = np.linalg.qr(rng.standard_normal((8, 8)))[0].astype(np.float32)
+    q = oracle.fdct(c1, T=Tc)
+    assert bits_equal(to_host(hp.inverse(to_dev(q, dev), transform=to_dev(Tc, dev))), oracle.idct(q, T=Tc))
+
+
+def test_golden_rt64(hp, dev, c1):
+    small = np.ascontiguousarray(c1[:64, :64])
+    a = to_host(hp.inverse(hp.forward(to_dev(small, dev), quantise=False), dequantise=False))
+    b = to_host(hp.inverse(hp.forward(to_dev(small, dev))))
+    assert bits_equal(a, np.load(os.path.join(GOLD, "rt64_unquant_f32.npy")))
+    assert bits_equal(b, np.load(os.path.join(GOLD, "rt64_quant_f32.npy")))
+
+
+# --------------------------------------------------------------------- compat surface
+def _flush_c_stdout():
+    ctypes.CDLL(None).fflush(None)
+
+
+def test_compat_entry_points(hp, oracle, dev, c1, capfd):
+    import torch
+    img = to_dev(c1.astype(np.float32), dev)
+    T = to_dev(hp.default_transform(), dev)
+    res = torch.empty_like(img)
+    hp.dct_all_blocks_cuda(img, 256, 256, T, res)
+    _flush_c_stdout()
+    q = oracle.fdct(c1)
+    assert bits_equal(to_host(res), q)
+    # the reference leaves X-128 in its input buffer (main_newAppr.cu:273)
+    assert np.array_equal(to_host(img), c1.astype(np.float32) - 128.0)
+    out = torch.empty_like(img)
+    hp.idct_all_blocks_cuda(res, 256, 256, T, out)
+    _flush_c_stdout()
+    assert bits_equal(to_host(out), oracle.idct(q))
+    text = capfd.readouterr().out
+    assert "DCT (256,256): " in text and "IDCT (256,256): " in text and " ms" in text
+
+
+# --------------------------------------------------------------------- generator
+@pytest.mark.parametrize("n,first", [(4096, 0), (1000, 12345), (17, 3)])
+def test_fill_hash_matches_oracle(hp, oracle, dev, n, first):
+    import torch
+    buf = torch.empty(n, dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(buf, 42, first)
+    assert np.array_equal(to_host(buf), oracle.hash_u8(n, 42, first))
+
+
+# --------------------------------------------------------------------- full-size configs
+def test_c2_1024_bitexact(hp, oracle, dev, golden):
+    img = oracle.rand_u8(1024 * 1024).reshape(1024, 1024)
+    q = to_host(hp.forward(to_dev(img, dev)))
+    assert sha(q) == golden["configs"]["c2_1024"]["q_f32_sha256"]
+    r = to_host(hp.inverse(to_dev(q, dev)))
+    assert sha(r) == golden["configs"]["c2_1024"]["roundtrip_f32_sha256"]
+
+
+def test_c3_8192_roundtrip(hp, oracle, dev, golden):
+    g = golden["configs"]["c3_8192"]
+    img = oracle.rand_u8(8192 * 8192).reshape(8192, 8192)
+    x = to_dev(img, dev)
+    qd = hp.forward(x)
+    q = to_host(qd)
+    assert sha(q) == g["q_f32_sha256"]
+    r = to_host(hp.inverse(qd))
+    assert sha(r) == g["roundtrip_f32_sha256"]
+    peen, mse = oracle.quality(img.astype(np.float32), r)
+    assert abs(mse - g["mse_f32"]) < 1e-6 and abs(peen - g["peen_f32"]) < 1e-6
+    assert 370 < mse < 380 and 12.9 < peen < 13.3
+    # size-independent properties at full size
+    c = hp.forward(x, quantise=False)
+    rt = hp.inverse(c, dequantise=False)
+    import torch
+    assert float((rt - x.float()).abs().max()) < 1e-4
+    assert float(qd.abs().max()) <= 98
