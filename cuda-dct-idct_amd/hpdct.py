@@ -72,6 +72,14 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    # libhpdct.so and torch both need libamdhip64.so.7 and the first one loaded
+    # wins the soname for the whole process.  Two HIP runtimes (torch's bundled
+    # copy and /opt/rocm's) in one process see no device, so let torch load
+    # its runtime first and bind the library to that same instance.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - host-only use without torch
+        pass
     if not os.path.exists(p):
         raise HpdctLibraryError(
             f"{p} not found: build it with `make -C cuda-dct-idct_amd` "

@@ -235,27 +235,42 @@ def test_golden_rt64(hp, dev, c1):
 
 
 # --------------------------------------------------------------------- compat surface
-def _flush_c_stdout():
-    ctypes.CDLL(None).fflush(None)
+_COMPAT_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [{pkg!r}, {orc!r}]
+import hpdct, oracle
+dev = torch.device("cuda:0")
+c1 = oracle.rand_u8(256 * 256, 42).reshape(256, 256)
+img = torch.from_numpy(c1.astype(np.float32)).to(dev)
+T = torch.from_numpy(hpdct.default_transform()).to(dev)
+res = torch.empty_like(img)
+hpdct.dct_all_blocks_cuda(img, 256, 256, T, res)
+q = oracle.fdct(c1)
+assert np.array_equal(res.cpu().numpy().view(np.uint32), q.view(np.uint32)), "forward"
+assert np.array_equal(img.cpu().numpy(), c1.astype(np.float32) - 128.0), "in-place X-128"
+out = torch.empty_like(img)
+hpdct.idct_all_blocks_cuda(res, 256, 256, T, out)
+assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.idct(q).view(np.uint32)), "inverse"
+bad = torch.empty((12, 16), device=dev)
+sys.stdout.flush()
+hpdct.dct_all_blocks_cuda(bad, 12, 16, T, torch.empty_like(bad))  # must print and exit(EXIT_FAILURE)
+print("NOT REACHED")
+"""
 
 
-def test_compat_entry_points(hp, oracle, dev, c1, capfd):
-    import torch
-    img = to_dev(c1.astype(np.float32), dev)
-    T = to_dev(hp.default_transform(), dev)
-    res = torch.empty_like(img)
-    hp.dct_all_blocks_cuda(img, 256, 256, T, res)
-    _flush_c_stdout()
-    q = oracle.fdct(c1)
-    assert bits_equal(to_host(res), q)
-    # the reference leaves X-128 in its input buffer (main_newAppr.cu:273)
-    assert np.array_equal(to_host(img), c1.astype(np.float32) - 128.0)
-    out = torch.empty_like(img)
-    hp.idct_all_blocks_cuda(res, 256, 256, T, out)
-    _flush_c_stdout()
-    assert bits_equal(to_host(out), oracle.idct(q))
-    text = capfd.readouterr().out
-    assert "DCT (256,256): " in text and "IDCT (256,256): " in text and " ms" in text
+def test_compat_entry_points():
+    """The reference-named C++ entry points (hpdct_compat.h) in a child
+    process: they print the timing line and exit() on error, like the
+    reference's CHECK_CUDA."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _COMPAT_SCRIPT.format(pkg=os.path.join(root, "cuda-dct-idct_amd"), orc=os.path.join(root, "oracle"))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 1, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    assert "DCT (256,256): " in p.stdout and "IDCT (256,256): " in p.stdout and " ms" in p.stdout
+    assert "not a positive multiple of 8" in p.stdout
+    assert "NOT REACHED" not in p.stdout and "AssertionError" not in p.stderr
 
 
 # --------------------------------------------------------------------- generator
