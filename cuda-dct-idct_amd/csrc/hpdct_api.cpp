@@ -21,6 +21,7 @@
 namespace {
 
 using hpdct::Mat64;
+using hpdct::QParams;
 using hpdct::TileGrid;
 
 // JPEG luminance table and the HpApprDCT matrix (main_newAppr.cu:60-81),
@@ -95,6 +96,23 @@ hpdct_status make_grid(int64_t height, int64_t width, TileGrid& g) {
     g.tiles_x = static_cast<uint32_t>(width / 8);
     g.width = static_cast<uint64_t>(width);
     return HPDCT_SUCCESS;
+}
+
+// The 3-operation quotient of the kernels gives the same roundf() as IEEE
+// C/Q for every |C| <= 4096 when Q is an integer in 1..255 (exhaustive on the
+// GPU: tests/tools/verify_fastdiv.hip, log in tests/tools/verify_fastdiv.gpu.log;
+// CPU cross-check for the JPEG table: tests/tools/verify_fastdiv.c).
+bool fastdiv_table(const Mat64& q) {
+    for (float v : q.v)
+        if (!(v >= 1.0f && v <= 255.0f) || v != std::floor(v)) return false;
+    return true;
+}
+
+QParams make_qparams(const Mat64& q) {
+    QParams p;
+    p.q = q;
+    for (int i = 0; i < 64; ++i) p.r.v[i] = 1.0f / q.v[i];  // RN(1/Q), as the verification tools compute it
+    return p;
 }
 
 bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
@@ -181,6 +199,9 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     const Mat64 q = current_q();
     if (out_type == HPDCT_I8 && !int8_safe(q))
         return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
+    const QParams qp = make_qparams(q);
+    // |C| <= 8*255 for uint8 input with the built-in T, well inside the verified |C| <= 4096
+    const bool fastdiv = quant && in_type == HPDCT_U8 && d_transform == nullptr && fastdiv_table(q);
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool bt = d_transform == nullptr;
@@ -188,11 +209,11 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     using namespace hpdct;
 #define FWD(TI, TO, QN, WB)                                                                                        \
     e = bt ? launch_fdct<TI, TO, QN, true, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),         \
-                                               static_cast<float*>(const_cast<void*>(d_image)), g, d_transform, q, \
-                                               shift, s)                                                           \
+                                               static_cast<float*>(const_cast<void*>(d_image)), g, d_transform,    \
+                                               qp, shift, fastdiv, s)                                              \
            : launch_fdct<TI, TO, QN, false, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),        \
                                                 static_cast<float*>(const_cast<void*>(d_image)), g, d_transform,   \
-                                                q, shift, s)
+                                                qp, shift, fastdiv, s)
     if (in_type == HPDCT_U8) {
         if (out_type == HPDCT_I8) {
             FWD(uint8_t, int8_t, true, false);

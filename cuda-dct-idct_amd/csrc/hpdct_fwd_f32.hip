@@ -3,9 +3,12 @@
 #include "hpdct_kernels_impl.hpp"
 
 namespace hpdct {
-#define HPDCT_FWD(TI, TO, QN, BT, WB)                                                                              \
-    template hipError_t launch_fdct<TI, TO, QN, BT, WB>(const TI*, TO*, float*, const TileGrid&, const float*,   \
-                                                        const Mat64&, float, hipStream_t);
+#define HPDCT_FWD(TI, TO, QN, BT, WB)                                                                       \
+    template <>                                                                                             \
+    hipError_t launch_fdct<TI, TO, QN, BT, WB>(const TI* a, TO* b, float* c, const TileGrid& g, const float* t, \
+                                               const QParams& q, float sh, bool fd, hipStream_t s) {        \
+        return launch_fdct_impl<TI, TO, QN, BT, WB>(a, b, c, g, t, q, sh, fd, s);                           \
+    }
 #define HPDCT_FWD_T(TI, TO, QN, WB) HPDCT_FWD(TI, TO, QN, true, WB) HPDCT_FWD(TI, TO, QN, false, WB)
 HPDCT_FWD_T(float, float, true, false)
 HPDCT_FWD_T(float, float, false, false)

@@ -2,9 +2,12 @@
 #include "hpdct_kernels_impl.hpp"
 
 namespace hpdct {
-#define HPDCT_INV(TI, TO, DQ, BT)                                                                                  \
-    template hipError_t launch_idct<TI, TO, DQ, BT>(const TI*, TO*, const TileGrid&, const float*, const Mat64&,  \
-                                                    float, hipStream_t);
+#define HPDCT_INV(TI, TO, DQ, BT)                                                                          \
+    template <>                                                                                             \
+    hipError_t launch_idct<TI, TO, DQ, BT>(const TI* a, TO* b, const TileGrid& g, const float* t,           \
+                                           const Mat64& q, float sh, hipStream_t s) {                       \
+        return launch_idct_impl<TI, TO, DQ, BT>(a, b, g, t, q, sh, s);                                      \
+    }
 #define HPDCT_INV_T(TI, TO, DQ) HPDCT_INV(TI, TO, DQ, true) HPDCT_INV(TI, TO, DQ, false)
 HPDCT_INV_T(float, float, true)
 HPDCT_INV_T(float, float, false)

@@ -1,5 +1,6 @@
 // hpdct_kernels.h -- host-visible declarations of the gfx950 kernels
-// (launchers are explicit template instantiations in hpdct_kernels.hip).
+// (launchers are explicit template instantiations in hpdct_fwd_*.hip /
+// hpdct_inv.hip; the kernels themselves are in hpdct_kernels_impl.hpp).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,6 +15,13 @@ struct Mat64 {
     float v[64];
 };
 
+// Quantiser parameters passed by value: Q and RN(1/Q) (the latter is used
+// only by the verified fast quotient).
+struct QParams {
+    Mat64 q;
+    Mat64 r;
+};
+
 // Tile geometry of one launch: ntiles = (height/8) * (width/8) < 2^32.
 struct TileGrid {
     uint32_t ntiles;
@@ -21,9 +29,12 @@ struct TileGrid {
     uint64_t width;  // elements per image row
 };
 
+// fastdiv: use the 3-operation quotient (only legal for uint8 input, the
+// built-in T and a table whose entries are all integers in 1..255; the
+// caller checks).  shift is 128 (reference level shift) or 0.
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                       const Mat64& q, float shift, hipStream_t s);
+                       const QParams& q, float shift, bool fastdiv, hipStream_t s);
 
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
 hipError_t launch_idct(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q, float shift,

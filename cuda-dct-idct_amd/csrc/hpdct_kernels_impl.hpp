@@ -2,15 +2,19 @@
 // CDNA4 (gfx950).  Replaces the three-launch chains of dct_all_blocks_cuda /
 // idct_all_blocks_cuda (main_newAppr.cu:252-332) with one HBM pass each.
 //
-// Mapping ("tile per lane"): lane L of the grid owns tile L of the image in
-// row-major tile order and keeps the whole 8x8 tile in VGPRs, so both passes
-// of T.X.T^T run in registers in the reference's exact FMA order with no
-// LDS traffic, no barrier and no cross-lane shuffles.  64 consecutive lanes
-// own 64 horizontally adjacent tiles, so
+// Mapping ("tile per lane"): lane L of a wave owns tile L of a 64-tile *set*
+// (64 horizontally adjacent tiles in row-major tile order) and keeps the whole
+// 8x8 tile in VGPRs, so both passes of T.X.T^T run in registers in the
+// reference's exact FMA order with no LDS traffic, no barrier and no
+// cross-lane shuffles.  Per set and wave:
 //   - each u8 row load is one global_load_dwordx2 covering 512 contiguous
-//     bytes per wave (8 per tile row set),
+//     bytes (8 per set),
 //   - each fp32 row store is two global_store_dwordx4 that together cover
-//     2 KiB contiguous per wave.
+//     2 KiB contiguous.
+// Persistent variant (kVarPersist): a grid of resident waves walks the sets
+// with stride = number of waves, and issues the loads of its next set before
+// computing the current one, so HBM reads overlap the VALU work instead of
+// every wave loading, then computing, then storing in lock-step.
 // Why not one wavefront per tile: a lane-per-pixel mapping needs 7 cross-lane
 // operands per output per pass (14 DPP/ds_bpermute per pixel), which on its
 // own costs as much LDS-crossbar time as the whole HBM stream; see DESIGN.md.
@@ -20,6 +24,22 @@
 #include "hpdct_tile.hpp"
 
 namespace hpdct {
+
+// Compile-time kernel variants (bit flags).
+enum : unsigned {
+    kVarFastDiv = 1u,  // quotient by  q0=c*r; e=fma(-q0,Q,c); q=fma(e,r,q0)  (r = RN(1/Q)).  Gives the same
+                       // roundf() as IEEE c/Q for every |c| <= 4096 and every integer Q in 1..255
+                       // (exhaustive: tests/tools/verify_fastdiv.*); only enabled for such tables and
+                       // uint8 input with the built-in T (|C| <= 1024).
+    kVarPersist = 2u,  // persistent waves + prefetch of the next tile set
+    kVarXorCvt = 4u,   // uint8 -> (x - 128) as (float)(int8_t)(b ^ 0x80): one XOR per 4 pixels + one
+                       // sign-extending byte convert per pixel instead of convert + subtract
+    kVarLdsStore = 8u, // fp32 rows re-staged through LDS so every store instruction writes 1 KiB contiguous
+    kVarNT = 16u,      // non-temporal (streaming) stores for the output planes
+    // bits 8..11: minimum waves per SIMD requested from the register allocator (0 = compiler default)
+};
+template <unsigned kVar>
+constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
 
 namespace {
 
@@ -43,13 +63,251 @@ __device__ __forceinline__ uint32_t pack_u8x4(float a, float b, float c, float d
     return to_u8(a) | (to_u8(b) << 8) | (to_u8(c) << 16) | (to_u8(d) << 24);
 }
 
-__device__ __forceinline__ bool tile_coords(const TileGrid& g, uint32_t& tile, uint64_t& base) {
-    tile = blockIdx.x * kBlockThreads + threadIdx.x;
-    if (tile >= g.ntiles) return false;
-    const uint32_t ty = tile / g.tiles_x;
-    const uint32_t tx = tile - ty * g.tiles_x;
-    base = static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(tx) * 8u;
-    return true;
+// roundf (round half away from zero) in three operations:
+//   trunc(x + copysign(0.49999997f, x))
+// bit-identical to roundf for all 2^32 fp32 inputs (NaN stays NaN); checked
+// exhaustively by tests/tools/verify_round3.c (tests/test_tools.py).
+__device__ __forceinline__ float round_half_away(float x) {
+    return __builtin_truncf(x + __builtin_copysignf(0.49999997f, x));
+}
+
+// divide_matrices (utils_kernels.cu:42): round(C / Q)
+template <unsigned kVar>
+__device__ __forceinline__ float quantise(float c, float q, float r) {
+    float d;
+    if constexpr (kVar & kVarFastDiv) {
+        const float q0 = c * r;
+        const float e = __builtin_fmaf(-q0, q, c);
+        d = __builtin_fmaf(e, r, q0);
+    } else {
+        (void)r;
+        d = c / q;  // IEEE (hipcc default: correctly rounded fp32 division)
+    }
+    return round_half_away(d);
+}
+
+// Tile-set geometry: lane's tile and the element offset of its top-left pixel.
+struct TilePos {
+    uint64_t base;
+    bool valid;
+};
+__device__ __forceinline__ TilePos tile_pos(const TileGrid& g, uint32_t tile) {
+    TilePos p;
+    p.valid = tile < g.ntiles;
+    const uint32_t t = p.valid ? tile : 0u;
+    const uint32_t ty = t / g.tiles_x;
+    const uint32_t tx = t - ty * g.tiles_x;
+    p.base = static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(tx) * 8u;
+    return p;
+}
+
+// ---- raw tile registers per input type ------------------------------------
+template <typename TIn>
+struct RawTile;
+
+template <>
+struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
+    uint2 r[8];
+    __device__ __forceinline__ void load(const uint8_t* __restrict__ p, uint64_t width) {
+        unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
+    }
+    __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
+        unroll<8>([&](auto i) {
+            unroll<4>([&](auto j) {
+                x[i][j] = byte_f32(r[i].x, j) - shift;
+                x[i][j + 4] = byte_f32(r[i].y, j) - shift;
+            });
+        });
+    }
+    // X - 128 exactly: (int8_t)(b ^ 0x80) == b - 128 for b in 0..255
+    __device__ __forceinline__ void to_float_minus128(float (&x)[8][8]) const {
+        unroll<8>([&](auto i) {
+            const uint32_t lo = r[i].x ^ 0x80808080u, hi = r[i].y ^ 0x80808080u;
+            unroll<4>([&](auto j) {
+                x[i][j] = static_cast<float>(static_cast<int32_t>(static_cast<int8_t>(lo >> (8 * j))));
+                x[i][j + 4] = static_cast<float>(static_cast<int32_t>(static_cast<int8_t>(hi >> (8 * j))));
+            });
+        });
+    }
+};
+
+template <>
+struct RawTile<int8_t> {  // int8 coefficients, 16 VGPRs
+    uint2 r[8];
+    __device__ __forceinline__ void load(const int8_t* __restrict__ p, uint64_t width) {
+        unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
+    }
+    __device__ __forceinline__ void to_float(float (&x)[8][8], float) const {
+        unroll<8>([&](auto i) {
+            unroll<4>([&](auto j) {
+                x[i][j] = static_cast<float>(static_cast<int8_t>((r[i].x >> (8 * j)) & 0xffu));
+                x[i][j + 4] = static_cast<float>(static_cast<int8_t>((r[i].y >> (8 * j)) & 0xffu));
+            });
+        });
+    }
+};
+
+template <>
+struct RawTile<float> {  // 64 VGPRs
+    float4 r[8][2];
+    __device__ __forceinline__ void load(const float* __restrict__ p, uint64_t width) {
+        unroll<8>([&](auto i) {
+            const float4* src = reinterpret_cast<const float4*>(p + i * width);
+            r[i][0] = src[0];
+            r[i][1] = src[1];
+        });
+    }
+    __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
+        unroll<8>([&](auto i) {
+            x[i][0] = r[i][0].x - shift;
+            x[i][1] = r[i][0].y - shift;
+            x[i][2] = r[i][0].z - shift;
+            x[i][3] = r[i][0].w - shift;
+            x[i][4] = r[i][1].x - shift;
+            x[i][5] = r[i][1].y - shift;
+            x[i][6] = r[i][1].z - shift;
+            x[i][7] = r[i][1].w - shift;
+        });
+    }
+};
+
+template <bool kNT>
+__device__ __forceinline__ void st(float4* p, const float4& v) {
+    if constexpr (kNT) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+template <bool kNT>
+__device__ __forceinline__ void st(uint2* p, const uint2& v) {
+    if constexpr (kNT) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+    } else {
+        *p = v;
+    }
+}
+
+// One output row of the lane's tile, written straight from the lane
+// (32 B per lane for fp32: two dwordx4 that cover 2 KiB per wave together).
+template <bool kNT, typename TOut>
+__device__ __forceinline__ void store_row(TOut* __restrict__ row, const float (&c)[8]) {
+    if constexpr (std::is_same_v<TOut, float>) {
+        float4* dst = reinterpret_cast<float4*>(row);
+        st<kNT>(dst, make_float4(c[0], c[1], c[2], c[3]));
+        st<kNT>(dst + 1, make_float4(c[4], c[5], c[6], c[7]));
+    } else if constexpr (std::is_same_v<TOut, int8_t>) {
+        st<kNT>(reinterpret_cast<uint2*>(row),
+                make_uint2(pack_i8x4(c[0], c[1], c[2], c[3]), pack_i8x4(c[4], c[5], c[6], c[7])));
+    } else {  // uint8 pixels: clamp + truncate
+        st<kNT>(reinterpret_cast<uint2*>(row),
+                make_uint2(pack_u8x4(c[0], c[1], c[2], c[3]), pack_u8x4(c[4], c[5], c[6], c[7])));
+    }
+}
+
+// fp32 row through a wave-private 2 KiB LDS slot: lane l deposits its 32 B
+// at [32l, 32l+32), then lane j stores [16j, 16j+16) and [1024+16j, ...) of
+// the 64-tile row segment starting at seg (= the row pixel of the set's
+// first tile), i.e. two stores of 1 KiB contiguous each.  LDS accesses of
+// one wave execute in order, so no barrier is needed between deposit and
+// pick-up; the slot alternates with the row parity to let them overlap.
+template <bool kNT>
+__device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* __restrict__ seg, uint32_t lane,
+                                              const float (&c)[8]) {
+    slot[2 * lane] = make_float4(c[0], c[1], c[2], c[3]);
+    slot[2 * lane + 1] = make_float4(c[4], c[5], c[6], c[7]);
+    const float4 a = slot[lane];
+    const float4 b = slot[64 + lane];
+    st<kNT>(reinterpret_cast<float4*>(seg) + lane, a);
+    st<kNT>(reinterpret_cast<float4*>(seg) + 64 + lane, b);
+}
+
+// Per-wave walk over 64-tile sets: one set per wave (plain), or a grid-stride
+// loop with the next set's loads issued before the current set's compute.
+// body(raw, p, seg_ok, seg): seg_ok (wave-uniform) says the whole set is 64
+// valid tiles of one tile row, whose row segments start at element seg.
+template <bool kPersist, typename TIn, typename Body>
+__device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, Body&& body) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64u) + threadIdx.x / 64u);
+    const uint32_t nsets = (g.ntiles + 63u) / 64u;
+    auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) {
+        const uint32_t t0 = set * 64u;
+        const bool ok = t0 + 63u < g.ntiles && (t0 / g.tiles_x) == ((t0 + 63u) / g.tiles_x);
+        seg = p.base - 8u * static_cast<uint64_t>(lane);
+        return ok;
+    };
+    if constexpr (!kPersist) {
+        if (wave >= nsets) return;
+        const TilePos p = tile_pos(g, wave * 64u + lane);
+        uint64_t seg;
+        const bool ok = seg_info(wave, p, seg);
+        if (!p.valid) return;
+        RawTile<TIn> raw;
+        raw.load(src + p.base, g.width);
+        body(raw, p, ok, seg);
+    } else {
+        const uint32_t nwaves = gridDim.x * (kBlockThreads / 64u);
+        uint32_t set = wave;
+        if (set >= nsets) return;
+        TilePos p = tile_pos(g, set * 64u + lane);
+        RawTile<TIn> cur;
+        if (p.valid) cur.load(src + p.base, g.width);
+        while (true) {
+            const uint32_t nset = set + nwaves;
+            const bool more = nset < nsets;  // wave-uniform
+            TilePos np = p;
+            RawTile<TIn> nxt;
+            if (more) {
+                np = tile_pos(g, nset * 64u + lane);
+                if (np.valid) nxt.load(src + np.base, g.width);
+            }
+            uint64_t seg;
+            const bool ok = seg_info(set, p, seg);
+            if (p.valid) body(cur, p, ok, seg);
+            if (!more) break;
+            cur = nxt;
+            p = np;
+            set = nset;
+        }
+    }
+}
+
+// Emits one row of 8 values for the lane's tile: through the LDS re-staging
+// (fp32 planes, whole 64-tile sets) or straight from the lane.
+template <unsigned kVar, typename TOut>
+struct RowSink {
+    static constexpr bool kNT = (kVar & kVarNT) != 0;
+    static constexpr bool kLds = (kVar & kVarLdsStore) != 0 && std::is_same_v<TOut, float>;
+    TOut* __restrict__ plane;
+    uint64_t width;
+    float4* slots;  // this wave's 2 x 128 float4 LDS slots (kLds)
+
+    template <typename V>
+    __device__ __forceinline__ void operator()(V v, const TilePos& p, bool seg_ok, uint64_t seg,
+                                               const float (&c)[8]) const {
+        if constexpr (kLds) {
+            if (seg_ok) {
+                store_row_lds<kNT>(slots + (v & 1) * 128, plane + seg + v * width, threadIdx.x & 63u, c);
+                return;
+            }
+        }
+        store_row<kNT>(plane + p.base + v * width, c);
+    }
+};
+
+template <unsigned kVar, typename TOut>
+__device__ __forceinline__ float4* wave_slots() {
+    if constexpr (RowSink<kVar, TOut>::kLds) {
+        __shared__ float4 stage[kBlockThreads / 64u][2 * 128];
+        return stage[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
+    } else {
+        return nullptr;
+    }
 }
 
 }  // namespace
@@ -57,131 +315,62 @@ __device__ __forceinline__ bool tile_coords(const TileGrid& g, uint32_t& tile, u
 // ---------------------------------------------------------------------------
 // Forward: image -> (quantised) coefficients.
 // ---------------------------------------------------------------------------
-template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
-__global__ __launch_bounds__(kBlockThreads) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
+template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
+__global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
                                                              float* __restrict__ shifted, TileGrid g,
-                                                             const float* __restrict__ t_dev, Mat64 q, float shift) {
-    uint32_t tile;
-    uint64_t base;
-    if (!tile_coords(g, tile, base)) return;
-
+                                                             const float* __restrict__ t_dev, QParams qp,
+                                                             float shift) {
     // finite inputs (u8) may skip the zero terms of the built-in T
     constexpr bool kSkipZero = std::is_same_v<TIn, uint8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
+    const RowSink<kVar, TOut> sink{out, g.width, wave_slots<kVar, TOut>()};
+    const RowSink<kVar, float> wb_sink{shifted, g.width, wave_slots<kVar, float>()};
 
-    float x[8][8];
-    if constexpr (std::is_same_v<TIn, uint8_t>) {
-        uint2 raw[8];
-        unroll<8>([&](auto i) { raw[i] = *reinterpret_cast<const uint2*>(img + base + i * g.width); });
-        unroll<8>([&](auto i) {
-            unroll<4>([&](auto j) {
-                x[i][j] = byte_f32(raw[i].x, j) - shift;
-                x[i][j + 4] = byte_f32(raw[i].y, j) - shift;
-            });
-        });
-    } else {
-        float4 raw[8][2];
-        unroll<8>([&](auto i) {
-            const float4* src = reinterpret_cast<const float4*>(img + base + i * g.width);
-            raw[i][0] = src[0];
-            raw[i][1] = src[1];
-        });
-        unroll<8>([&](auto i) {
-            x[i][0] = raw[i][0].x - shift;
-            x[i][1] = raw[i][0].y - shift;
-            x[i][2] = raw[i][0].z - shift;
-            x[i][3] = raw[i][0].w - shift;
-            x[i][4] = raw[i][1].x - shift;
-            x[i][5] = raw[i][1].y - shift;
-            x[i][6] = raw[i][1].z - shift;
-            x[i][7] = raw[i][1].w - shift;
-        });
+    walk_sets<(kVar & kVarPersist) != 0>(img, g, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+                                                      uint64_t seg) {
+        float x[8][8];
+        if constexpr ((kVar & kVarXorCvt) != 0 && std::is_same_v<TIn, uint8_t>) {
+            raw.to_float_minus128(x);  // launcher guarantees shift == 128
+        } else {
+            raw.to_float(x, shift);
+        }
         if constexpr (kWriteback) {
             // the reference leaves X-128 in its input (main_newAppr.cu:273)
-            unroll<8>([&](auto i) {
-                float4* dst = reinterpret_cast<float4*>(shifted + base + i * g.width);
-                dst[0] = make_float4(x[i][0], x[i][1], x[i][2], x[i][3]);
-                dst[1] = make_float4(x[i][4], x[i][5], x[i][6], x[i][7]);
-            });
+            unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
         }
-    }
-
-    fdct_tile(T, x, [&](auto v, float (&c)[8]) {
-        if constexpr (kQuant) {
-            // divide_matrices (utils_kernels.cu:42): round(C / Q[v][u])
-            unroll<8>([&](auto u) { c[u] = __builtin_roundf(c[u] / q.v[v * 8 + u]); });
-        }
-        TOut* row = out + base + v * g.width;
-        if constexpr (std::is_same_v<TOut, float>) {
-            float4* dst = reinterpret_cast<float4*>(row);
-            dst[0] = make_float4(c[0], c[1], c[2], c[3]);
-            dst[1] = make_float4(c[4], c[5], c[6], c[7]);
-        } else {
-            *reinterpret_cast<uint2*>(row) = make_uint2(pack_i8x4(c[0], c[1], c[2], c[3]),
-                                                        pack_i8x4(c[4], c[5], c[6], c[7]));
-        }
+        fdct_tile(T, x, [&](auto v, float (&c)[8]) {
+            if constexpr (kQuant) {
+                unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+            }
+            sink(v, p, ok, seg, c);
+        });
     });
 }
 
 // ---------------------------------------------------------------------------
 // Inverse: (quantised) coefficients -> image.
 // ---------------------------------------------------------------------------
-template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-__global__ __launch_bounds__(kBlockThreads) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
+template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT, unsigned kVar>
+__global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
                                                              TileGrid g, const float* __restrict__ t_dev, Mat64 q,
                                                              float shift) {
-    uint32_t tile;
-    uint64_t base;
-    if (!tile_coords(g, tile, base)) return;
-
     constexpr bool kSkipZero = std::is_same_v<TIn, int8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
+    const RowSink<kVar, TOut> sink{out, g.width, wave_slots<kVar, TOut>()};
 
-    float d[8][8];
-    if constexpr (std::is_same_v<TIn, int8_t>) {
-        uint2 raw[8];
-        unroll<8>([&](auto i) { raw[i] = *reinterpret_cast<const uint2*>(coef + base + i * g.width); });
-        unroll<8>([&](auto i) {
-            unroll<4>([&](auto j) {
-                d[i][j] = static_cast<float>(static_cast<int8_t>((raw[i].x >> (8 * j)) & 0xffu));
-                d[i][j + 4] = static_cast<float>(static_cast<int8_t>((raw[i].y >> (8 * j)) & 0xffu));
-            });
-        });
-    } else {
-        float4 raw[8][2];
-        unroll<8>([&](auto i) {
-            const float4* src = reinterpret_cast<const float4*>(coef + base + i * g.width);
-            raw[i][0] = src[0];
-            raw[i][1] = src[1];
-        });
-        unroll<8>([&](auto i) {
-            d[i][0] = raw[i][0].x;
-            d[i][1] = raw[i][0].y;
-            d[i][2] = raw[i][0].z;
-            d[i][3] = raw[i][0].w;
-            d[i][4] = raw[i][1].x;
-            d[i][5] = raw[i][1].y;
-            d[i][6] = raw[i][1].z;
-            d[i][7] = raw[i][1].w;
-        });
-    }
-    if constexpr (kDequant) {
-        // multiply_matrices (utils_kernels.cu:55): D = q * Q[i][j]
-        unroll<8>([&](auto i) { unroll<8>([&](auto j) { d[i][j] = d[i][j] * q.v[i * 8 + j]; }); });
-    }
-
-    idct_tile(T, d, [&](auto v, float (&r)[8]) {
-        // add_matrix_scalar (utils_kernels.cu:29): R + 128, no clamp
-        unroll<8>([&](auto u) { r[u] = r[u] + shift; });
-        TOut* row = out + base + v * g.width;
-        if constexpr (std::is_same_v<TOut, float>) {
-            float4* dst = reinterpret_cast<float4*>(row);
-            dst[0] = make_float4(r[0], r[1], r[2], r[3]);
-            dst[1] = make_float4(r[4], r[5], r[6], r[7]);
-        } else {
-            *reinterpret_cast<uint2*>(row) =
-                make_uint2(pack_u8x4(r[0], r[1], r[2], r[3]), pack_u8x4(r[4], r[5], r[6], r[7]));
+    walk_sets<(kVar & kVarPersist) != 0>(coef, g, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+                                                       uint64_t seg) {
+        float d[8][8];
+        raw.to_float(d, 0.0f);
+        if constexpr (kDequant) {
+            // multiply_matrices (utils_kernels.cu:55): D = q * Q[i][j]
+            unroll<8>([&](auto i) { unroll<8>([&](auto j) { d[i][j] = d[i][j] * q.v[i * 8 + j]; }); });
         }
+        idct_tile(T, d, [&](auto v, float (&r)[8]) {
+            // add_matrix_scalar (utils_kernels.cu:29): R + 128, no clamp
+            unroll<8>([&](auto u) { r[u] = r[u] + shift; });
+            sink(v, p, ok, seg, r);
+        });
     });
 }
 
@@ -196,7 +385,7 @@ __device__ __forceinline__ uint32_t hash_px(uint64_t seed, uint64_t idx) {
 }
 
 static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t* __restrict__ out, uint64_t n,
-                                                                  uint64_t seed, uint64_t first) {
+                                                                         uint64_t seed, uint64_t first) {
     const uint64_t i0 = (static_cast<uint64_t>(blockIdx.x) * kBlockThreads + threadIdx.x) * 16u;
     if (i0 >= n) return;
     if (i0 + 16 <= n) {
@@ -213,25 +402,67 @@ static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t
 }
 
 // ---------------------------------------------------------------------------
-// Launchers (host side).  Shapes are validated by the caller (hpdct_api.hip).
+// Launch geometry.
 // ---------------------------------------------------------------------------
-namespace {
-inline dim3 grid_for(const TileGrid& g) { return dim3((g.ntiles + kBlockThreads - 1) / kBlockThreads); }
-}  // namespace
+// Resident waves per CU the persistent kernels are sized for (4 waves/SIMD at
+// <= 128 VGPRs); 256 CUs on MI355X.  The grid never exceeds the set count.
+constexpr uint32_t kPersistWavesPerCU = 16;
+
+inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u;
+    const uint32_t waves_per_block = kBlockThreads / 64u;
+    uint32_t blocks = (sets + waves_per_block - 1) / waves_per_block;
+    if (persist) {
+        const uint32_t cap = cus * kPersistWavesPerCU / waves_per_block;
+        if (blocks > cap) blocks = cap;
+    }
+    return dim3(blocks);
+}
+
+inline uint32_t device_cus() {
+    static thread_local int cached_dev = -1;
+    static thread_local uint32_t cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev != cached_dev) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            cached_cus = static_cast<uint32_t>(cus);
+        cached_dev = dev;
+    }
+    return cached_cus;
+}
+
+// Product variant choice (measured on MI355X, tools/kbench.hip):
+// fp32 planes are stored through the LDS re-staging with non-temporal
+// stores (1 KiB contiguous per store instruction), 8-bit planes with
+// non-temporal stores; the fast quotient where the caller proved it legal.
+template <typename TOut>
+constexpr unsigned kStoreVar = std::is_same_v<TOut, float> ? (kVarLdsStore | kVarNT) : kVarNT;
 
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
-hipError_t launch_fdct(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                       const Mat64& q, float shift, hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback>), grid_for(g), dim3(kBlockThreads), 0,
-                       s, img, out, shifted, g, t_dev, q, shift);
+hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
+                            const QParams& q, float shift, bool fastdiv, hipStream_t s) {
+    constexpr unsigned kBase = kStoreVar<TOut>;
+    const dim3 grid = grid_for(g, false, 0);
+    if constexpr (std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback) {
+        if (fastdiv) {
+            hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase | kVarFastDiv>), grid,
+                               dim3(kBlockThreads), 0, s, img, out, shifted, g, t_dev, q, shift);
+            return hipGetLastError();
+        }
+    }
+    (void)fastdiv;
+    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase>), grid, dim3(kBlockThreads), 0, s,
+                       img, out, shifted, g, t_dev, q, shift);
     return hipGetLastError();
 }
 
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-hipError_t launch_idct(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q, float shift,
-                       hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT>), grid_for(g), dim3(kBlockThreads), 0, s, coef,
-                       out, g, t_dev, q, shift);
+hipError_t launch_idct_impl(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q,
+                            float shift, hipStream_t s) {
+    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kStoreVar<TOut>>), grid_for(g, false, 0),
+                       dim3(kBlockThreads), 0, s, coef, out, g, t_dev, q, shift);
     return hipGetLastError();
 }
 

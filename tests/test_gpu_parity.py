@@ -116,6 +116,25 @@ def test_custom_transform_and_quant(hp, oracle, dev, c1):
     assert bits_equal(builtin, oracle.fdct(c1, Q=Q))
 
 
+@pytest.mark.parametrize("qtab", ["fractional", "large", "ones", "max255"])
+def test_quant_table_paths(hp, oracle, dev, c1, qtab):
+    """Integer tables in 1..255 take the verified 3-op quotient, anything else
+    IEEE division: both must equal the oracle (IEEE C/Q) bit for bit."""
+    rng = np.random.default_rng(11)
+    Q = {"fractional": rng.uniform(1.0, 50.0, (8, 8)),
+         "large": rng.integers(200, 5000, (8, 8)),
+         "ones": np.ones((8, 8)),
+         "max255": np.full((8, 8), 255.0)}[qtab].astype(np.float32)
+    hp.set_quant_table(Q)
+    try:
+        got = to_host(hp.forward(to_dev(c1, dev)))
+        got_nq = to_host(hp.forward(to_dev(np.full((16, 16), 255, np.uint8), dev)))
+    finally:
+        hp.set_quant_table(None)
+    assert bits_equal(got, oracle.fdct(c1, Q=Q))
+    assert bits_equal(got_nq, oracle.fdct(np.full((16, 16), 255, np.uint8), Q=Q))
+
+
 @pytest.mark.parametrize("h,w", [(8, 8), (8, 16), (16, 8), (24, 40), (8, 4096), (520, 8), (1000, 1008), (72, 2056)])
 def test_forward_shapes(hp, oracle, dev, h, w):
     img = np.random.default_rng(h * 7919 + w).integers(0, 256, (h, w), dtype=np.uint8)

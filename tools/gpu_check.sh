@@ -25,5 +25,5 @@ rc=$?; [ $rc -le 1 ] || exit $rc
 step bench 600 python bench.py "$@" || exit $?
 cd /tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o hpdct -- \
-    python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline || exit $?
+    python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-extras || exit $?
 echo ALLDONE

@@ -1,0 +1,211 @@
+// membench.hip -- development micro-benchmark of the HBM ceilings that bound
+// the DCT kernels on MI355X: pure read, pure write, and the 1-B-in / 4-B-out
+// streaming mix of the uint8 -> fp32 forward pass, with plain and
+// non-temporal stores, several per-lane widths and grid sizes.  Buffers
+// rotate over > 1 GB so the 256 MiB Infinity Cache does not serve them.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(2);                                                                 \
+        }                                                                            \
+    } while (0)
+
+__device__ __forceinline__ float4 cvt4(uint32_t w) {
+    return make_float4((float)(w & 255u), (float)((w >> 8) & 255u), (float)((w >> 16) & 255u), (float)(w >> 24));
+}
+
+template <bool kNT>
+__device__ __forceinline__ void st4(float4* p, float4 v) {
+    if constexpr (kNT) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+
+// 1 B in -> 4 B out, each lane 4 px per step (1 KiB contiguous store per wave-instr)
+template <bool kNT>
+__global__ __launch_bounds__(256) void mix_w4(const uint32_t* __restrict__ in, float4* __restrict__ out, uint64_t n4) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n4; i += stride) st4<kNT>(&out[i], cvt4(in[i]));
+}
+
+// 16 px per lane per step: 1 uint4 load, 4 float4 stores, each store instruction 1 KiB contiguous
+template <bool kNT>
+__global__ __launch_bounds__(256) void mix_w16(const uint4* __restrict__ in, float4* __restrict__ out, uint64_t n16) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * 4u;
+    for (uint64_t c = wave; c * 64u < n16; c += nw) {  // chunk of 64 uint4 = 1 KiB in, 4 KiB out
+        const uint64_t j = c * 64u + lane;
+        if (j >= n16) break;
+        const uint4 w = in[j];
+        // output of chunk c: 256 float4; the lane's 4 float4 are at 4*lane..4*lane+3 in the natural layout;
+        // re-map so each store instruction k covers float4 [64k, 64k+64) contiguously.
+        // value for position p = 64k + lane comes from lane p/4, word p%4 -> shuffle via ds_bpermute.
+        uint32_t words[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = 64 * k + (int)lane;
+            const int src_lane = p >> 2;
+            const int word = p & 3;
+            uint32_t v0 = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)words[0]);
+            uint32_t v1 = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)words[1]);
+            uint32_t v2 = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)words[2]);
+            uint32_t v3 = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)words[3]);
+            const uint32_t v = word == 0 ? v0 : word == 1 ? v1 : word == 2 ? v2 : v3;
+            st4<kNT>(&out[c * 256u + p], cvt4(v));
+        }
+    }
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(256) void write_only(float4* __restrict__ out, uint64_t n4) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n4; i += stride)
+        st4<kNT>(&out[i], make_float4((float)i, 1.f, 2.f, 3.f));
+}
+
+__global__ __launch_bounds__(256) void read_only(const uint4* __restrict__ in, uint64_t n16, uint32_t* sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n16; i += stride) {
+        const uint4 w = in[i];
+        acc ^= w.x ^ w.y ^ w.z ^ w.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// tile pattern (the DCT kernel's): per lane 8 rows x (8 B in, 32 B out)
+template <bool kNT>
+__global__ __launch_bounds__(256) void tile_mix(const uint8_t* __restrict__ in, float* __restrict__ out, uint32_t ntiles,
+                                                uint32_t tiles_x, uint64_t width) {
+    const uint32_t tile = blockIdx.x * 256u + threadIdx.x;
+    if (tile >= ntiles) return;
+    const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const uint64_t base = (uint64_t)ty * 8u * width + (uint64_t)tx * 8u;
+    uint2 r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint2*>(in + base + i * width);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float4* d = reinterpret_cast<float4*>(out + base + i * width);
+        st4<kNT>(d, cvt4(r[i].x));
+        st4<kNT>(d + 1, cvt4(r[i].y));
+    }
+}
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 8192;
+    const int iters = argc > 2 ? atoi(argv[2]) : 40;
+    const int nsets = 4;
+    const size_t px = (size_t)n * n;
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<uint8_t*> in(nsets);
+    std::vector<float*> out(nsets);
+    for (int s = 0; s < nsets; ++s) {
+        CK(hipMalloc(&in[s], px));
+        CK(hipMalloc(&out[s], px * 4));
+        CK(hipMemset(in[s], s + 1, px));
+    }
+    uint32_t* sink;
+    CK(hipMalloc(&sink, 64));
+    struct Case {
+        std::string name;
+        double bytes;
+        std::function<void(int)> run;
+    };
+    std::vector<Case> cases;
+    const uint64_t n4 = px / 4, n16 = px / 16;
+    for (int gm : {4, 8, 16, 32}) {
+        const unsigned grid = cus * gm;
+        cases.push_back({"mix_w4 plain g" + std::to_string(gm), 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(mix_w4<false>, dim3(grid), dim3(256), 0, 0,
+                                                (const uint32_t*)in[s], (float4*)out[s], n4);
+                         }});
+        cases.push_back({"mix_w4 nt    g" + std::to_string(gm), 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(mix_w4<true>, dim3(grid), dim3(256), 0, 0, (const uint32_t*)in[s],
+                                                (float4*)out[s], n4);
+                         }});
+    }
+    for (int gm : {4, 8, 16}) {
+        const unsigned grid = cus * gm;
+        cases.push_back({"mix_w16 plain g" + std::to_string(gm), 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(mix_w16<false>, dim3(grid), dim3(256), 0, 0, (const uint4*)in[s],
+                                                (float4*)out[s], n16);
+                         }});
+        cases.push_back({"mix_w16 nt    g" + std::to_string(gm), 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(mix_w16<true>, dim3(grid), dim3(256), 0, 0, (const uint4*)in[s],
+                                                (float4*)out[s], n16);
+                         }});
+    }
+    const uint32_t ntiles = px / 64, tiles_x = n / 8;
+    cases.push_back({"tile_mix plain", 5.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(tile_mix<false>, dim3((ntiles + 255) / 256), dim3(256), 0, 0, in[s],
+                                            out[s], ntiles, tiles_x, (uint64_t)n);
+                     }});
+    cases.push_back({"tile_mix nt", 5.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(tile_mix<true>, dim3((ntiles + 255) / 256), dim3(256), 0, 0, in[s],
+                                            out[s], ntiles, tiles_x, (uint64_t)n);
+                     }});
+    for (int gm : {8, 16}) {
+        const unsigned grid = cus * gm;
+        cases.push_back({"write_only plain g" + std::to_string(gm), 4.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(write_only<false>, dim3(grid), dim3(256), 0, 0, (float4*)out[s], n4);
+                         }});
+        cases.push_back({"write_only nt    g" + std::to_string(gm), 4.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(write_only<true>, dim3(grid), dim3(256), 0, 0, (float4*)out[s], n4);
+                         }});
+        cases.push_back({"read_only 4B/px  g" + std::to_string(gm), 4.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(read_only, dim3(grid), dim3(256), 0, 0, (const uint4*)out[s], n4 / 1,
+                                                sink);
+                         }});
+    }
+    cases.push_back({"hipMemcpyD2D 4B/px (r+w)", 8.0 * px, [=](int s) {
+                         CK(hipMemcpyAsync(out[s], out[(s + 1) % nsets], px * 4, hipMemcpyDeviceToDevice, 0));
+                     }});
+    cases.push_back({"hipMemsetD32 4B/px", 4.0 * px, [=](int s) { CK(hipMemsetD32Async((hipDeviceptr_t)out[s], 7, px, 0)); }});
+
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<std::vector<float>> us(cases.size());
+    for (int r = 0; r < 3; ++r)
+        for (size_t c = 0; c < cases.size(); ++c) {
+            for (int w = 0; w < 3; ++w) cases[c].run(w % nsets);
+            for (int i = 0; i < iters; ++i) {
+                CK(hipEventRecord(a, 0));
+                cases[c].run(i % nsets);
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                us[c].push_back(ms * 1e3f);
+            }
+        }
+    printf("%-30s %10s %10s %10s %7s\n", "case", "median_us", "min_us", "GB/s", "frac8T");
+    for (size_t c = 0; c < cases.size(); ++c) {
+        auto t = us[c];
+        std::sort(t.begin(), t.end());
+        const double med = t[t.size() / 2];
+        const double gbs = cases[c].bytes / (med * 1e-6) / 1e9;
+        printf("%-30s %10.2f %10.2f %10.1f %7.3f\n", cases[c].name.c_str(), med, t[0], gbs, gbs / 8000.0);
+    }
+    return 0;
+}
