@@ -1,0 +1,82 @@
+"""Row-sharded multi-rank path (hpdct_dist) on CPU with the gloo backend.
+
+The N>1 bench path shards a frame into 8-row-aligned slabs, runs the forward
+kernel per slab on each GPU and gathers the coefficient slabs to rank 0 (RCCL
+on the GPU node).  Here the same shard/gather code runs over gloo with
+world_size 2 and 3; each rank computes its slab with the CPU oracle (the
+checker: there is no GPU in this container) and rank 0 checks that the
+gathered frame equals the oracle's unsharded result bit for bit.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-dct-idct_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from hpdct_dist import all_shards, shard_rows  # noqa: E402
+
+
+@pytest.mark.parametrize("height,world", [(8, 1), (64, 2), (72, 2), (16384, 8), (8192, 3), (40, 8), (800, 7)])
+def test_shard_rows_partition(height, world):
+    shards = all_shards(height, world)
+    assert shards[0][0] == 0
+    for (r0, rows), (n0, _) in zip(shards, shards[1:]):
+        assert n0 == r0 + rows
+    assert shards[-1][0] + shards[-1][1] == height
+    assert all(r0 % 8 == 0 and rows % 8 == 0 for r0, rows in shards)
+    sizes = [rows for _, rows in shards]
+    assert max(sizes) - min(sizes) <= 8
+
+
+def test_shard_rows_rejects_bad_input():
+    with pytest.raises(ValueError):
+        shard_rows(12, 2, 0)
+    with pytest.raises(ValueError):
+        shard_rows(16, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, height, width, result_path):
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from hpdct_dist import gather_slabs, shard_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r0, rows = shard_rows(height, world, rank)
+        # same stateless generator the bench uses on the device (C4)
+        slab = oracle.hash_u8(rows * width, seed=42, first_index=r0 * width).reshape(rows, width)
+        coef = torch.from_numpy(oracle.fdct(slab))
+        full = gather_slabs(coef, height, width, root=0)
+        if rank == 0:
+            ref = oracle.fdct(oracle.hash_u8(height * width, seed=42).reshape(height, width))
+            ok = np.array_equal(full.numpy().view(np.uint32), ref.view(np.uint32))
+            with open(result_path, "w") as fh:
+                fh.write("ok" if ok else "mismatch")
+        else:
+            assert full is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height,width", [(2, 64, 96), (2, 72, 40), (3, 80, 64)])
+def test_sharded_gather_equals_unsharded(tmp_path, world, height, width):
+    import torch.multiprocessing as mp
+    result = tmp_path / "result.txt"
+    mp.spawn(_worker, args=(world, _free_port(), height, width, str(result)), nprocs=world, join=True)
+    assert result.read_text() == "ok"

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <functional>
@@ -90,6 +91,19 @@ __global__ __launch_bounds__(256) void read_only(const uint4* __restrict__ in, u
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// calibration kernels for the PMC byte counters (known byte counts, the
+// access widths of the DCT kernels: dwordx2 loads, dwordx4 loads, dwordx4
+// non-temporal stores)
+__global__ __launch_bounds__(256) void calib_read_x2(const uint2* __restrict__ in, uint64_t n8, uint32_t* sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n8; i += stride) {
+        const uint2 w = in[i];
+        acc ^= w.x ^ w.y;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 // tile pattern (the DCT kernel's): per lane 8 rows x (8 B in, 32 B out)
 template <bool kNT>
 __global__ __launch_bounds__(256) void tile_mix(const uint8_t* __restrict__ in, float* __restrict__ out, uint32_t ntiles,
@@ -109,7 +123,38 @@ __global__ __launch_bounds__(256) void tile_mix(const uint8_t* __restrict__ in, 
     }
 }
 
+static int calib(int cus) {
+    // 256 MiB buffers, each kernel 5 times: FETCH_SIZE / WRITE_SIZE per
+    // dispatch divided by these byte counts = the counter's calibration
+    const size_t bytes = 256ull << 20;
+    void *a, *b;
+    uint32_t* sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(a, 1, bytes));
+    CK(hipMemset(b, 2, bytes));
+    for (int i = 0; i < 5; ++i) {
+        hipLaunchKernelGGL(calib_read_x2, dim3(cus * 8), dim3(256), 0, 0, (const uint2*)(i & 1 ? a : b), bytes / 8,
+                           sink);
+        hipLaunchKernelGGL(read_only, dim3(cus * 8), dim3(256), 0, 0, (const uint4*)(i & 1 ? a : b), bytes / 16,
+                           sink);
+        hipLaunchKernelGGL(write_only<true>, dim3(cus * 8), dim3(256), 0, 0, (float4*)(i & 1 ? a : b), bytes / 16);
+        hipLaunchKernelGGL(write_only<false>, dim3(cus * 8), dim3(256), 0, 0, (float4*)(i & 1 ? b : a), bytes / 16);
+    }
+    CK(hipDeviceSynchronize());
+    printf("calibration kernels: 5 x {calib_read_x2, read_only(x4), write_only nt, write_only plain}, "
+           "%zu bytes each\n", bytes);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "calib") == 0) {
+        int dev = 0, cus = 0;
+        CK(hipGetDevice(&dev));
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        return calib(cus);
+    }
     const int n = argc > 1 ? atoi(argv[1]) : 8192;
     const int iters = argc > 2 ? atoi(argv[2]) : 40;
     const int nsets = 4;
