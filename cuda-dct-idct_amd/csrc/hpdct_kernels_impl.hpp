@@ -36,10 +36,19 @@ enum : unsigned {
                        // sign-extending byte convert per pixel instead of convert + subtract
     kVarLdsStore = 8u, // fp32 rows re-staged through LDS so every store instruction writes 1 KiB contiguous
     kVarNT = 16u,      // non-temporal (streaming) stores for the output planes
+    kVarRowMajor = 32u,  // forward: finish each P row and its C row before the next (fewer live VGPRs?)
+    kVarLdsSwz = 64u,    // LDS re-staging with the slot swizzle k ^ ((k >> 3) & 1): conflict-free deposits
+    kVarLdsLoad = 128u,  // fp32 inputs: 1 KiB-contiguous row loads, re-staged through LDS into the tile layout
     // bits 8..11: minimum waves per SIMD requested from the register allocator (0 = compiler default)
+    // bits 12..13: workgroup size: 0 -> 256 threads, 1 -> 64, 2 -> 512, 3 -> 1024
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
+template <unsigned kVar>
+constexpr uint32_t kBlock = ((kVar >> 12) & 3u) == 1u   ? 64u
+                            : ((kVar >> 12) & 3u) == 2u ? 512u
+                            : ((kVar >> 12) & 3u) == 3u ? 1024u
+                                                        : kBlockThreads;
 
 namespace {
 
@@ -157,6 +166,26 @@ struct RawTile<float> {  // 64 VGPRs
             r[i][1] = src[1];
         });
     }
+    // Whole 64-tile set in one tile row: lane j loads 16 B at [16j, 16j+16) and
+    // [1024+16j, ...) of each 2 KiB row segment (two 1 KiB-contiguous loads per
+    // row), the rows pass through the wave's LDS slots and every lane picks up
+    // its own tile's 32 B.  In-order LDS within one wave: no barrier.
+    __device__ __forceinline__ void load_staged(const float* __restrict__ seg, uint64_t width, uint32_t lane,
+                                                float4* __restrict__ slots) {
+        float4 a[8], b[8];
+        unroll<8>([&](auto i) {
+            const float4* src = reinterpret_cast<const float4*>(seg + i * width);
+            a[i] = src[lane];
+            b[i] = src[64 + lane];
+        });
+        unroll<8>([&](auto i) {
+            float4* slot = slots + (i & 1) * 128;
+            slot[lane] = a[i];
+            slot[64 + lane] = b[i];
+            r[i][0] = slot[2 * lane];
+            r[i][1] = slot[2 * lane + 1];
+        });
+    }
     __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
         unroll<8>([&](auto i) {
             x[i][0] = r[i][0].x - shift;
@@ -215,25 +244,30 @@ __device__ __forceinline__ void store_row(TOut* __restrict__ row, const float (&
 // first tile), i.e. two stores of 1 KiB contiguous each.  LDS accesses of
 // one wave execute in order, so no barrier is needed between deposit and
 // pick-up; the slot alternates with the row parity to let them overlap.
-template <bool kNT>
+// Optional slot swizzle sw(k) = k ^ ((k >> 3) & 1) (an involution that keeps
+// [0,64) and [64,128)): the deposits of 8 consecutive lanes then hit 8
+// distinct 16-B bank groups; the pick-up of slot j stores to position sw(j).
+template <bool kNT, bool kSwz>
 __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* __restrict__ seg, uint32_t lane,
                                               const float (&c)[8]) {
-    slot[2 * lane] = make_float4(c[0], c[1], c[2], c[3]);
-    slot[2 * lane + 1] = make_float4(c[4], c[5], c[6], c[7]);
+    auto sw = [](uint32_t k) { return kSwz ? (k ^ ((k >> 3) & 1u)) : k; };
+    slot[sw(2 * lane)] = make_float4(c[0], c[1], c[2], c[3]);
+    slot[sw(2 * lane + 1)] = make_float4(c[4], c[5], c[6], c[7]);
     const float4 a = slot[lane];
     const float4 b = slot[64 + lane];
-    st<kNT>(reinterpret_cast<float4*>(seg) + lane, a);
-    st<kNT>(reinterpret_cast<float4*>(seg) + 64 + lane, b);
+    st<kNT>(reinterpret_cast<float4*>(seg) + sw(lane), a);
+    st<kNT>(reinterpret_cast<float4*>(seg) + 64 + sw(lane), b);
 }
 
 // Per-wave walk over 64-tile sets: one set per wave (plain), or a grid-stride
 // loop with the next set's loads issued before the current set's compute.
 // body(raw, p, seg_ok, seg): seg_ok (wave-uniform) says the whole set is 64
 // valid tiles of one tile row, whose row segments start at element seg.
-template <bool kPersist, typename TIn, typename Body>
-__device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, Body&& body) {
+template <unsigned kVar, typename TIn, typename Body>
+__device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, float4* slots, Body&& body) {
+    constexpr bool kPersist = (kVar & kVarPersist) != 0;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64u) + threadIdx.x / 64u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t nsets = (g.ntiles + 63u) / 64u;
     auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) {
         const uint32_t t0 = set * 64u;
@@ -248,10 +282,18 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         const bool ok = seg_info(wave, p, seg);
         if (!p.valid) return;
         RawTile<TIn> raw;
-        raw.load(src + p.base, g.width);
+        if constexpr ((kVar & kVarLdsLoad) != 0 && std::is_same_v<TIn, float>) {
+            if (ok) {
+                raw.load_staged(src + seg, g.width, lane, slots);
+            } else {
+                raw.load(src + p.base, g.width);
+            }
+        } else {
+            raw.load(src + p.base, g.width);
+        }
         body(raw, p, ok, seg);
     } else {
-        const uint32_t nwaves = gridDim.x * (kBlockThreads / 64u);
+        const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
         uint32_t set = wave;
         if (set >= nsets) return;
         TilePos p = tile_pos(g, set * 64u + lane);
@@ -292,7 +334,8 @@ struct RowSink {
                                                const float (&c)[8]) const {
         if constexpr (kLds) {
             if (seg_ok) {
-                store_row_lds<kNT>(slots + (v & 1) * 128, plane + seg + v * width, threadIdx.x & 63u, c);
+                store_row_lds<kNT, (kVar & kVarLdsSwz) != 0>(slots + (v & 1) * 128, plane + seg + v * width,
+                                                             threadIdx.x & 63u, c);
                 return;
             }
         }
@@ -300,10 +343,11 @@ struct RowSink {
     }
 };
 
-template <unsigned kVar, typename TOut>
+// The wave's two 2 KiB LDS slots (used by the store and load re-staging).
+template <unsigned kVar>
 __device__ __forceinline__ float4* wave_slots() {
-    if constexpr (RowSink<kVar, TOut>::kLds) {
-        __shared__ float4 stage[kBlockThreads / 64u][2 * 128];
+    if constexpr ((kVar & (kVarLdsStore | kVarLdsLoad)) != 0) {
+        __shared__ float4 stage[kBlock<kVar> / 64u][2 * 128];
         return stage[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
     } else {
         return nullptr;
@@ -316,17 +360,18 @@ __device__ __forceinline__ float4* wave_slots() {
 // Forward: image -> (quantised) coefficients.
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
-__global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
+__global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
                                                              float* __restrict__ shifted, TileGrid g,
                                                              const float* __restrict__ t_dev, QParams qp,
                                                              float shift) {
     // finite inputs (u8) may skip the zero terms of the built-in T
     constexpr bool kSkipZero = std::is_same_v<TIn, uint8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
-    const RowSink<kVar, TOut> sink{out, g.width, wave_slots<kVar, TOut>()};
-    const RowSink<kVar, float> wb_sink{shifted, g.width, wave_slots<kVar, float>()};
+    float4* const slots = wave_slots<kVar>();
+    const RowSink<kVar, TOut> sink{out, g.width, slots};
+    const RowSink<kVar, float> wb_sink{shifted, g.width, slots};
 
-    walk_sets<(kVar & kVarPersist) != 0>(img, g, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
                                                       uint64_t seg) {
         float x[8][8];
         if constexpr ((kVar & kVarXorCvt) != 0 && std::is_same_v<TIn, uint8_t>) {
@@ -338,7 +383,7 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void fdct_kernel(co
             // the reference leaves X-128 in its input (main_newAppr.cu:273)
             unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
         }
-        fdct_tile(T, x, [&](auto v, float (&c)[8]) {
+        fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, [&](auto v, float (&c)[8]) {
             if constexpr (kQuant) {
                 unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
             }
@@ -351,14 +396,15 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void fdct_kernel(co
 // Inverse: (quantised) coefficients -> image.
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT, unsigned kVar>
-__global__ __launch_bounds__(kBlockThreads, kMinWaves<kVar>) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
+__global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
                                                              TileGrid g, const float* __restrict__ t_dev, Mat64 q,
                                                              float shift) {
     constexpr bool kSkipZero = std::is_same_v<TIn, int8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
-    const RowSink<kVar, TOut> sink{out, g.width, wave_slots<kVar, TOut>()};
+    float4* const slots = wave_slots<kVar>();
+    const RowSink<kVar, TOut> sink{out, g.width, slots};
 
-    walk_sets<(kVar & kVarPersist) != 0>(coef, g, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+    walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
                                                        uint64_t seg) {
         float d[8][8];
         raw.to_float(d, 0.0f);
@@ -408,9 +454,9 @@ static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t
 // <= 128 VGPRs); 256 CUs on MI355X.  The grid never exceeds the set count.
 constexpr uint32_t kPersistWavesPerCU = 16;
 
-inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus) {
+inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t block = kBlockThreads) {
     const uint32_t sets = (g.ntiles + 63u) / 64u;
-    const uint32_t waves_per_block = kBlockThreads / 64u;
+    const uint32_t waves_per_block = block / 64u;
     uint32_t blocks = (sets + waves_per_block - 1) / waves_per_block;
     if (persist) {
         const uint32_t cap = cus * kPersistWavesPerCU / waves_per_block;
@@ -437,32 +483,36 @@ inline uint32_t device_cus() {
 // fp32 planes are stored through the LDS re-staging with non-temporal
 // stores (1 KiB contiguous per store instruction), 8-bit planes with
 // non-temporal stores; the fast quotient where the caller proved it legal.
-template <typename TOut>
-constexpr unsigned kStoreVar = std::is_same_v<TOut, float> ? (kVarLdsStore | kVarNT) : kVarNT;
+// All product kernels use 512-thread workgroups (2u << 12: measured 1-3 %
+// faster than 256 on every kernel of the path, tools/kbench.hip).
+template <typename TIn, typename TOut>
+constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u);
 
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                             const QParams& q, float shift, bool fastdiv, hipStream_t s) {
-    constexpr unsigned kBase = kStoreVar<TOut>;
-    const dim3 grid = grid_for(g, false, 0);
+    constexpr unsigned kBase = kProdVar<TIn, TOut>;
+    constexpr uint32_t kB = kBlock<kBase>;
+    const dim3 grid = grid_for(g, false, 0, kB);
     if constexpr (std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback) {
         if (fastdiv) {
             hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase | kVarFastDiv>), grid,
-                               dim3(kBlockThreads), 0, s, img, out, shifted, g, t_dev, q, shift);
+                               dim3(kB), 0, s, img, out, shifted, g, t_dev, q, shift);
             return hipGetLastError();
         }
     }
     (void)fastdiv;
-    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase>), grid, dim3(kBlockThreads), 0, s,
-                       img, out, shifted, g, t_dev, q, shift);
+    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase>), grid, dim3(kB), 0, s, img, out,
+                       shifted, g, t_dev, q, shift);
     return hipGetLastError();
 }
 
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
 hipError_t launch_idct_impl(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q,
                             float shift, hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kStoreVar<TOut>>), grid_for(g, false, 0),
-                       dim3(kBlockThreads), 0, s, coef, out, g, t_dev, q, shift);
+    constexpr unsigned kV = kProdVar<TIn, TOut>;
+    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), grid_for(g, false, 0, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, coef, out, g, t_dev, q, shift);
     return hipGetLastError();
 }
 

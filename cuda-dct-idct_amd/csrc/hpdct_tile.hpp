@@ -110,8 +110,26 @@ struct TSource {
 // Forward tile transform on registers: x[i][j] level-shifted pixels,
 // returns P via the column pass, then calls emit(v, c[8]) for each output row
 // (so each row can be quantised and stored while the next is computed).
-template <typename TS, typename Emit>
+template <bool kRowMajor = false, typename TS, typename Emit>
 __device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& emit) {
+    if constexpr (kRowMajor) {
+        // same chains, P row v and C row v finished before row v+1
+        unroll<8>([&](auto v) {
+            float p[8], c[8];
+            unroll<8>([&](auto col) {
+                float s = 0.0f;
+                unroll<8>([&](auto i) { s = T.template mac<v * 8 + i>(x[i][col], s); });
+                p[col] = s;
+            });
+            unroll<8>([&](auto u) {
+                float s = 0.0f;
+                unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(p[i], s); });
+                c[u] = s;
+            });
+            emit(v, c);
+        });
+        return;
+    }
     float p[8][8];
     // P = T . X   (main_newAppr.cu:193-197): P[v][col] = sum_i T[v][i] X[i][col]
     unroll<8>([&](auto col) {

@@ -59,12 +59,13 @@ __global__ __launch_bounds__(256) void copy_linear(const uint32_t* __restrict__ 
 struct Variant {
     std::string name;
     void (*launch)(const uint8_t*, float*, const TileGrid&, const QParams&, uint32_t cus, hipStream_t);
+    bool f32_input = false;  // reads the fp32 frame set instead of the uint8 one
 };
 
 template <unsigned kVar>
 void launch_var(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus, hipStream_t s) {
-    const dim3 grid = grid_for(g, (kVar & kVarPersist) != 0, cus);
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), grid, dim3(kBlockThreads), 0, s, in,
+    const dim3 grid = grid_for(g, (kVar & kVarPersist) != 0, cus, kBlock<kVar>);
+    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), grid, dim3(kBlock<kVar>), 0, s, in,
                        out, nullptr, g, nullptr, qp, 128.0f);
 }
 
@@ -82,14 +83,16 @@ void launch_var_occ(const uint8_t* in, float* out, const TileGrid& g, const QPar
 template <typename TI, typename TO, unsigned kVar>
 void launch_fwd_any(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                     hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, false, cus), dim3(kBlockThreads),
+    hipLaunchKernelGGL((fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, false, cus, kBlock<kVar>),
+                       dim3(kBlock<kVar>),
                        0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr, g, nullptr, qp,
                        128.0f);
 }
 template <typename TI, typename TO, unsigned kVar>
 void launch_inv_any(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                     hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<TI, TO, true, true, kVar>), grid_for(g, false, cus), dim3(kBlockThreads), 0, s,
+    hipLaunchKernelGGL((idct_kernel<TI, TO, true, true, kVar>), grid_for(g, false, cus, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), g, nullptr, qp.q, 128.0f);
 }
 
@@ -120,7 +123,7 @@ int main(int argc, char** argv) {
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
 
-    std::vector<uint8_t*> in(nsets);
+    std::vector<uint8_t*> in(nsets), inf(nsets);
     std::vector<float*> out(nsets);
     std::vector<uint8_t> h(px);
     srand(42);
@@ -130,26 +133,26 @@ int main(int argc, char** argv) {
         CK(hipMemset(in[s], 0, px * 4));
         CK(hipMalloc(&out[s], px * 4));
         CK(hipMemcpy(in[s], h.data(), px, hipMemcpyHostToDevice));
+        // fp32 frames (pixel values 0..255 as float) for the fp32-input kernels
+        std::vector<float> hf(px);
+        for (size_t i = 0; i < px; ++i) hf[i] = (float)h[(i * 7919u + s) % px];
+        CK(hipMalloc(&inf[s], px * 4));
+        CK(hipMemcpy(inf[s], hf.data(), px * 4, hipMemcpyHostToDevice));
     }
     constexpr unsigned F = kVarFastDiv, X = kVarXorCvt, L = kVarLdsStore, N = kVarNT, P = kVarPersist;
+    constexpr unsigned B = L | N | F, R = kVarRowMajor, S = kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
+    constexpr unsigned LL = kVarLdsLoad;
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
-        {"plain", launch_var<0>},
-        {"lds+nt", launch_var<L | N>},
-        {"lds+nt+fast", launch_var<L | N | F>},
-        {"lds+nt+fast+xor", launch_var<L | N | F | X>},
+        {"product (b512+lds+nt+fast)", launch_var<B | W512>},
     };
-    // secondary kernels: timed only (bytes column assumes 5 B/px; see names for the real B/px)
     std::vector<Variant> other = {
-        {"fwd u8->i8 fast+nt (2B/px)", launch_fwd_any<uint8_t, int8_t, F | N>},
-        {"fwd u8->i8 fast+nt+xor (2B/px)", launch_fwd_any<uint8_t, int8_t, F | N | X>},
-        {"fwd f32->f32 (8B/px)", launch_fwd_any<float, float, 0>},
-        {"fwd f32->f32 lds+nt (8B/px)", launch_fwd_any<float, float, L | N>},
-        {"inv f32->f32 (8B/px)", launch_inv_any<float, float, 0>},
-        {"inv f32->f32 lds+nt (8B/px)", launch_inv_any<float, float, L | N>},
-        {"inv i8->u8 (2B/px)", launch_inv_any<int8_t, uint8_t, 0>},
-        {"inv i8->u8 nt (2B/px)", launch_inv_any<int8_t, uint8_t, N>},
-        {"inv i8->f32 lds+nt (5B/px)", launch_inv_any<int8_t, float, L | N>},
+        {"fwd f32->f32 lds+nt b512 (8B/px)", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32->f32 +ldsload", launch_fwd_any<float, float, L | N | W512 | LL>, true},
+        {"inv f32->f32 lds+nt b512 (8B/px)", launch_inv_any<float, float, L | N | W512>, true},
+        {"inv f32->f32 +ldsload", launch_inv_any<float, float, L | N | W512 | LL>, true},
+        {"fwd f32->f32 plain b256", launch_fwd_any<float, float, 0>, true},
+        {"fwd f32->f32 nt-only b512", launch_fwd_any<float, float, N | W512>, true},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
@@ -165,6 +168,22 @@ int main(int argc, char** argv) {
         printf("check %-32s %s\n", vars[v].name.c_str(), ok ? "bit-exact" : "MISMATCH");
         if (!ok) return 1;
     }
+    // pairs (other[2k], other[2k+1]) must agree bit for bit on a real fp32 frame (in[1])
+    for (size_t v = 0; v + 1 < other.size(); v += 2) {
+        CK(hipMemset(out[2], 0xab, px * 4));
+        CK(hipMemset(out[3], 0xcd, px * 4));
+        other[v].launch(other[v].f32_input ? inf[1] : in[1], out[2], g, qp, cus, 0);
+        other[v + 1].launch(other[v + 1].f32_input ? inf[1] : in[1], out[3], g, qp, cus, 0);
+        CK(hipDeviceSynchronize());
+        std::vector<uint8_t> A(px * 4), Bv(px * 4);
+        CK(hipMemcpy(A.data(), out[2], px * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(Bv.data(), out[3], px * 4, hipMemcpyDeviceToHost));
+        const size_t nb = other[v].name.find("->u8") != std::string::npos ? px : px * 4;
+        const bool ok = memcmp(A.data(), Bv.data(), nb) == 0;
+        printf("check %-32s == %-24s %s\n", other[v + 1].name.c_str(), other[v].name.c_str(),
+               ok ? "bit-exact" : "MISMATCH");
+        if (!ok) return 1;
+    }
     vars.insert(vars.end(), other.begin(), other.end());
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -172,10 +191,11 @@ int main(int argc, char** argv) {
     std::vector<std::vector<float>> us(vars.size());
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vars.size(); ++v) {
-            for (int w = 0; w < 5; ++w) vars[v].launch(in[w % nsets], out[w % nsets], g, qp, cus, 0);
+            auto src = [&](int i) { return vars[v].f32_input ? inf[i % nsets] : in[i % nsets]; };
+            for (int w = 0; w < 5; ++w) vars[v].launch(src(w), out[w % nsets], g, qp, cus, 0);
             for (int i = 0; i < iters; ++i) {
                 CK(hipEventRecord(a, 0));
-                vars[v].launch(in[i % nsets], out[i % nsets], g, qp, cus, 0);
+                vars[v].launch(src(i), out[i % nsets], g, qp, cus, 0);
                 CK(hipEventRecord(b, 0));
                 CK(hipEventSynchronize(b));
                 float ms = 0;
@@ -183,6 +203,17 @@ int main(int argc, char** argv) {
                 us[v].push_back(ms * 1e3f);
             }
         }
+    }
+    for (size_t v = 0; v < vars.size(); ++v) {
+        printf("per-set median %-32s", vars[v].name.c_str());
+        for (int st = 0; st < nsets; ++st) {
+            std::vector<float> t;
+            for (size_t k = 0; k < us[v].size(); ++k)
+                if ((int)((k % iters) % nsets) == st) t.push_back(us[v][k]);
+            std::sort(t.begin(), t.end());
+            printf(" %8.2f", t[t.size() / 2]);
+        }
+        printf("\n");
     }
     printf("%-34s %10s %10s %10s %8s\n", "variant", "median_us", "min_us", "GB/s(5B)", "frac8T");
     for (size_t v = 0; v < vars.size(); ++v) {
