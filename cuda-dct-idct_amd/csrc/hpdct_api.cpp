@@ -172,8 +172,8 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     TileGrid g;
     if (hpdct_status st = make_grid(height, width, g)) return st;
     if (!d_image || !d_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "null image or coefficient pointer");
-    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_WRITEBACK_SHIFT | HPDCT_FLAG_NO_SHIFT))
-        return fail(HPDCT_ERROR_UNSUPPORTED, "unknown flag bits");
+    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_WRITEBACK_SHIFT | HPDCT_FLAG_NO_SHIFT | HPDCT_FLAG_ROW_FIRST))
+        return fail(HPDCT_ERROR_UNSUPPORTED, "unknown or inverse-only flag bits");
     if (in_type != HPDCT_U8 && in_type != HPDCT_F32)
         return fail(HPDCT_ERROR_UNSUPPORTED, "forward input must be HPDCT_U8 or HPDCT_F32");
     if (out_type != HPDCT_F32 && out_type != HPDCT_I8)
@@ -183,6 +183,9 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     const float shift = (flags & HPDCT_FLAG_NO_SHIFT) ? 0.0f : 128.0f;
     if (wb && in_type != HPDCT_F32)
         return fail(HPDCT_ERROR_UNSUPPORTED, "HPDCT_FLAG_WRITEBACK_SHIFT needs an fp32 input");
+    const bool row_first = (flags & HPDCT_FLAG_ROW_FIRST) != 0;
+    if (row_first && (in_type != HPDCT_F32 || out_type != HPDCT_F32))
+        return fail(HPDCT_ERROR_UNSUPPORTED, "HPDCT_FLAG_ROW_FIRST is the fp32 -> fp32 (cublasDCTv2) path");
     if (out_type == HPDCT_I8) {
         if (!quant) return fail(HPDCT_ERROR_UNSUPPORTED, "int8 output needs quantisation");
         if (in_type != HPDCT_U8 || d_transform || shift != 128.0f)
@@ -210,10 +213,10 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
 #define FWD(TI, TO, QN, WB)                                                                                        \
     e = bt ? launch_fdct<TI, TO, QN, true, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),         \
                                                static_cast<float*>(const_cast<void*>(d_image)), g, d_transform,    \
-                                               qp, shift, fastdiv, s)                                              \
+                                               qp, shift, fastdiv, row_first, s)                                   \
            : launch_fdct<TI, TO, QN, false, WB>(static_cast<const TI*>(d_image), static_cast<TO*>(d_coef),        \
                                                 static_cast<float*>(const_cast<void*>(d_image)), g, d_transform,   \
-                                                qp, shift, fastdiv, s)
+                                                qp, shift, fastdiv, row_first, s)
     if (in_type == HPDCT_U8) {
         if (out_type == HPDCT_I8) {
             FWD(uint8_t, int8_t, true, false);
@@ -242,7 +245,7 @@ hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_imag
     TileGrid g;
     if (hpdct_status st = make_grid(height, width, g)) return st;
     if (!d_image || !d_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "null image or coefficient pointer");
-    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_NO_SHIFT))
+    if (flags & ~(HPDCT_FLAG_NO_QUANT | HPDCT_FLAG_NO_SHIFT | HPDCT_FLAG_ROW_FIRST | HPDCT_FLAG_WRITEBACK_DEQUANT))
         return fail(HPDCT_ERROR_UNSUPPORTED, "unknown or forward-only flag bits");
     if (in_type != HPDCT_F32 && in_type != HPDCT_I8)
         return fail(HPDCT_ERROR_UNSUPPORTED, "inverse input must be HPDCT_F32 or HPDCT_I8");
@@ -258,16 +261,22 @@ hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_imag
         return fail(HPDCT_ERROR_INVALID_VALUE, "coefficient and image buffers overlap");
     const bool deq = !(flags & HPDCT_FLAG_NO_QUANT);
     const float shift = (flags & HPDCT_FLAG_NO_SHIFT) ? 0.0f : 128.0f;
+    const bool row_first = (flags & HPDCT_FLAG_ROW_FIRST) != 0;
+    const bool wb = (flags & HPDCT_FLAG_WRITEBACK_DEQUANT) != 0;
+    if ((row_first || wb) && (in_type != HPDCT_F32 || out_type != HPDCT_F32))
+        return fail(HPDCT_ERROR_UNSUPPORTED, "ROW_FIRST / WRITEBACK_DEQUANT are fp32 -> fp32 (cublasDCTv2) options");
+    if (wb && !deq) return fail(HPDCT_ERROR_UNSUPPORTED, "HPDCT_FLAG_WRITEBACK_DEQUANT needs dequantisation");
+    float* dq_out = wb ? static_cast<float*>(const_cast<void*>(d_coef)) : nullptr;
     const Mat64 q = current_q();
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool bt = d_transform == nullptr;
     hipError_t e = hipSuccess;
     using namespace hpdct;
 #define INV(TI, TO, DQ)                                                                                           \
-    e = bt ? launch_idct<TI, TO, DQ, true>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), g,         \
-                                           d_transform, q, shift, s)                                             \
-           : launch_idct<TI, TO, DQ, false>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), g,        \
-                                            d_transform, q, shift, s)
+    e = bt ? launch_idct<TI, TO, DQ, true>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), dq_out, g, \
+                                           d_transform, q, shift, row_first, s)                                  \
+           : launch_idct<TI, TO, DQ, false>(static_cast<const TI*>(d_coef), static_cast<TO*>(d_image), dq_out, g,\
+                                            d_transform, q, shift, row_first, s)
 #define INV_Q(TI, TO)          \
     if (deq) {                 \
         INV(TI, TO, true);     \

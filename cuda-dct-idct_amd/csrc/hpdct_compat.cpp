@@ -79,3 +79,27 @@ void idct_all_blocks_cuda(const float* image_matrix, const int img_height, const
                      __LINE__);
     });
 }
+
+// cublasDCTv2 surface (main_cublass_2.cu:197-252): row pass first, X-128 left
+// in image_matrix, result = round((T.(X-128).T^T)/Q).  The handle is unused.
+void dct_all_blocks(float* image_matrix, const int img_height, const int img_width, const float* transform_matrix,
+                    float* result, cublasContext* /*handle*/) {
+    check_shape(img_height, img_width);
+    timed("DCT", img_width, img_height, [&] {
+        check_status(hpdct_forward(image_matrix, HPDCT_F32, result, HPDCT_F32, img_height, img_width,
+                                   transform_matrix, HPDCT_FLAG_WRITEBACK_SHIFT | HPDCT_FLAG_ROW_FIRST, nullptr),
+                     __LINE__);
+    });
+}
+
+// main_cublass_2.cu:257-311: q*Q left in image_matrix (in-place
+// multiply_matrices, :285), result = T^T.(q*Q).T + 128 with D.T computed first.
+void idct_all_blocks(float* image_matrix, const int img_height, const int img_width, const float* transform_matrix,
+                     float* result, cublasContext* /*handle*/) {
+    check_shape(img_height, img_width);
+    timed("IDCT", img_width, img_height, [&] {
+        check_status(hpdct_inverse(image_matrix, HPDCT_F32, result, HPDCT_F32, img_height, img_width,
+                                   transform_matrix, HPDCT_FLAG_ROW_FIRST | HPDCT_FLAG_WRITEBACK_DEQUANT, nullptr),
+                     __LINE__);
+    });
+}

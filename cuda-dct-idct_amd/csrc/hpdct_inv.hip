@@ -4,9 +4,9 @@
 namespace hpdct {
 #define HPDCT_INV(TI, TO, DQ, BT)                                                                          \
     template <>                                                                                             \
-    hipError_t launch_idct<TI, TO, DQ, BT>(const TI* a, TO* b, const TileGrid& g, const float* t,           \
-                                           const Mat64& q, float sh, hipStream_t s) {                       \
-        return launch_idct_impl<TI, TO, DQ, BT>(a, b, g, t, q, sh, s);                                      \
+    hipError_t launch_idct<TI, TO, DQ, BT>(const TI* a, TO* b, float* w, const TileGrid& g, const float* t,  \
+                                           const Mat64& q, float sh, bool rf, hipStream_t s) {              \
+        return launch_idct_impl<TI, TO, DQ, BT>(a, b, w, g, t, q, sh, rf, s);                               \
     }
 #define HPDCT_INV_T(TI, TO, DQ) HPDCT_INV(TI, TO, DQ, true) HPDCT_INV(TI, TO, DQ, false)
 HPDCT_INV_T(float, float, true)

@@ -32,13 +32,16 @@ struct TileGrid {
 // fastdiv: use the 3-operation quotient (only legal for uint8 input, the
 // built-in T and a table whose entries are all integers in 1..255; the
 // caller checks).  shift is 128 (reference level shift) or 0.
+// row_first: cublasDCTv2 pass order (fp32 -> fp32 only).
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                       const QParams& q, float shift, bool fastdiv, hipStream_t s);
+                       const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s);
 
+// dq_out (fp32 -> fp32 with dequantisation only, else nullptr): q*Q is also
+// written there (the in-place multiply of the cublasDCTv2 inverse).
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-hipError_t launch_idct(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q, float shift,
-                       hipStream_t s);
+hipError_t launch_idct(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
+                       const Mat64& q, float shift, bool row_first, hipStream_t s);
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 

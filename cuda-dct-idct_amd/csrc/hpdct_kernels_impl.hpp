@@ -41,6 +41,9 @@ enum : unsigned {
     kVarLdsLoad = 128u,  // fp32 inputs: 1 KiB-contiguous row loads, re-staged through LDS into the tile layout
     // bits 8..11: minimum waves per SIMD requested from the register allocator (0 = compiler default)
     // bits 12..13: workgroup size: 0 -> 256 threads, 1 -> 64, 2 -> 512, 3 -> 1024
+    kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
+    kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
+                              // (in-place multiply_matrices of main_cublass_2.cu:285)
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
@@ -383,12 +386,17 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
             // the reference leaves X-128 in its input (main_newAppr.cu:273)
             unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
         }
-        fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, [&](auto v, float (&c)[8]) {
+        auto emit = [&](auto v, float (&c)[8]) {
             if constexpr (kQuant) {
                 unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
             }
             sink(v, p, ok, seg, c);
-        });
+        };
+        if constexpr ((kVar & kVarRowFirst) != 0) {
+            fdct_tile_rowfirst(T, x, emit);
+        } else {
+            fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, emit);
+        }
     });
 }
 
@@ -397,12 +405,13 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT, unsigned kVar>
 __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
-                                                             TileGrid g, const float* __restrict__ t_dev, Mat64 q,
-                                                             float shift) {
+                                                             float* __restrict__ dq_out, TileGrid g,
+                                                             const float* __restrict__ t_dev, Mat64 q, float shift) {
     constexpr bool kSkipZero = std::is_same_v<TIn, int8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, TOut> sink{out, g.width, slots};
+    const RowSink<kVar, float> dq_sink{dq_out, g.width, slots};
 
     walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
                                                        uint64_t seg) {
@@ -411,12 +420,20 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(con
         if constexpr (kDequant) {
             // multiply_matrices (utils_kernels.cu:55): D = q * Q[i][j]
             unroll<8>([&](auto i) { unroll<8>([&](auto j) { d[i][j] = d[i][j] * q.v[i * 8 + j]; }); });
+            if constexpr ((kVar & kVarWbDequant) != 0) {
+                unroll<8>([&](auto i) { dq_sink(i, p, ok, seg, d[i]); });
+            }
         }
-        idct_tile(T, d, [&](auto v, float (&r)[8]) {
+        auto emit = [&](auto v, float (&r)[8]) {
             // add_matrix_scalar (utils_kernels.cu:29): R + 128, no clamp
             unroll<8>([&](auto u) { r[u] = r[u] + shift; });
             sink(v, p, ok, seg, r);
-        });
+        };
+        if constexpr ((kVar & kVarRowFirst) != 0) {
+            idct_tile_rowfirst(T, d, emit);
+        } else {
+            idct_tile(T, d, emit);
+        }
     });
 }
 
@@ -488,32 +505,60 @@ inline uint32_t device_cus() {
 template <typename TIn, typename TOut>
 constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u);
 
+template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev, const QParams& q,
+                   float shift, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>), grid_for(g, false, 0, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, img, out, shifted, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                            const QParams& q, float shift, bool fastdiv, hipStream_t s) {
+                            const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
     constexpr unsigned kBase = kProdVar<TIn, TOut>;
-    constexpr uint32_t kB = kBlock<kBase>;
-    const dim3 grid = grid_for(g, false, 0, kB);
     if constexpr (std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback) {
-        if (fastdiv) {
-            hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase | kVarFastDiv>), grid,
-                               dim3(kB), 0, s, img, out, shifted, g, t_dev, q, shift);
-            return hipGetLastError();
-        }
+        if (fastdiv)
+            return fdct_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
+                                                                                          q, shift, s);
+    }
+    if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
+        if (row_first)
+            return fdct_go<kBase | kVarRowFirst, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
+                                                                                           t_dev, q, shift, s);
     }
     (void)fastdiv;
-    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kBase>), grid, dim3(kB), 0, s, img, out,
-                       shifted, g, t_dev, q, shift);
+    (void)row_first;
+    return fdct_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+}
+
+template <unsigned kV, typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
+hipError_t idct_go(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev, const Mat64& q,
+                   float shift, hipStream_t s) {
+    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), grid_for(g, false, 0, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, coef, out, dq_out, g, t_dev, q, shift);
     return hipGetLastError();
 }
 
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-hipError_t launch_idct_impl(const TIn* coef, TOut* out, const TileGrid& g, const float* t_dev, const Mat64& q,
-                            float shift, hipStream_t s) {
+hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
+                            const Mat64& q, float shift, bool row_first, hipStream_t s) {
     constexpr unsigned kV = kProdVar<TIn, TOut>;
-    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), grid_for(g, false, 0, kBlock<kV>),
-                       dim3(kBlock<kV>), 0, s, coef, out, g, t_dev, q, shift);
-    return hipGetLastError();
+    if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
+        if constexpr (kDequant) {
+            if (dq_out && row_first)
+                return idct_go<kV | kVarRowFirst | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g,
+                                                                                                 t_dev, q, shift, s);
+            if (dq_out)
+                return idct_go<kV | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q,
+                                                                                   shift, s);
+        }
+        if (row_first)
+            return idct_go<kV | kVarRowFirst, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
+                                                                              s);
+    }
+    (void)row_first;
+    return idct_go<kV, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
 }
 
 inline hipError_t launch_fill_hash_impl(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {

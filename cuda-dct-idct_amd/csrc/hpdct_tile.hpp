@@ -151,6 +151,52 @@ __device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& 
     });
 }
 
+// cublasDCTv2 pass order (main_cublass_2.cu:228-235): R = X.T^T (row pass,
+// temp1) first, then C = T.R, each a sequential FMA chain over the 8
+// non-trivial terms of the block-diagonal GEMM's k range.
+template <typename TS, typename Emit>
+__device__ __forceinline__ void fdct_tile_rowfirst(const TS& T, float (&x)[8][8], Emit&& emit) {
+    float r[8][8];
+    unroll<8>([&](auto i) {
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto j) { s = T.template mac<u * 8 + j>(x[i][j], s); });
+            r[i][u] = s;
+        });
+    });
+    unroll<8>([&](auto v) {
+        float c[8];
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<v * 8 + i>(r[i][u], s); });
+            c[u] = s;
+        });
+        emit(v, c);
+    });
+}
+
+// cublasDCTv2 inverse order (main_cublass_2.cu:288-295): R = D.T, then T^T.R.
+template <typename TS, typename Emit>
+__device__ __forceinline__ void idct_tile_rowfirst(const TS& T, float (&d)[8][8], Emit&& emit) {
+    float r[8][8];
+    unroll<8>([&](auto i) {
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto j) { s = T.template mac<j * 8 + u>(d[i][j], s); });
+            r[i][u] = s;
+        });
+    });
+    unroll<8>([&](auto v) {
+        float c[8];
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<i * 8 + v>(r[i][u], s); });
+            c[u] = s;
+        });
+        emit(v, c);
+    });
+}
+
 // Inverse tile transform: d[i][j] dequantised coefficients.
 template <typename TS, typename Emit>
 __device__ __forceinline__ void idct_tile(const TS& T, float (&d)[8][8], Emit&& emit) {

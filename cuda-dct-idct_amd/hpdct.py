@@ -29,6 +29,8 @@ U8, I8, F32 = 0, 1, 2
 FLAG_NO_QUANT = 0x1
 FLAG_WRITEBACK_SHIFT = 0x2
 FLAG_NO_SHIFT = 0x4
+FLAG_ROW_FIRST = 0x8
+FLAG_WRITEBACK_DEQUANT = 0x10
 
 STATUS = {
     0: "HPDCT_SUCCESS",
@@ -50,6 +52,9 @@ C_SYMBOLS = [
 COMPAT_SYMBOLS = {
     "dct_all_blocks_cuda": "_Z19dct_all_blocks_cudaPfiiPKfS_",
     "idct_all_blocks_cuda": "_Z20idct_all_blocks_cudaPKfiiS0_Pf",
+    # cublasDCTv2 surface (main_cublass_2.cu:36-37); last argument: cublasHandle_t (ignored)
+    "dct_all_blocks": "_Z14dct_all_blocksPfiiPKfS_P13cublasContext",
+    "idct_all_blocks": "_Z15idct_all_blocksPfiiPKfS_P13cublasContext",
 }
 
 
@@ -114,7 +119,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_f32_to_u8.restype = None
     for name, mangled in COMPAT_SYMBOLS.items():
         f = getattr(lib, mangled)
-        f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+        f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp] + ([vp] if not name.endswith("_cuda") else [])
         f.restype = None
     if path is None:
         _lib = lib
@@ -195,7 +200,7 @@ def _hw(t, height, width):
 
 
 def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, writeback_shift=False,
-            level_shift=True, height=None, width=None, stream=None):
+            level_shift=True, row_first=False, height=None, width=None, stream=None):
     """Fused forward pass on the GPU: round((T.(X-128).T^T)/Q) per 8x8 tile.
 
     image: CUDA tensor, uint8 or float32, (..., H, W) contiguous (a stack of
@@ -208,7 +213,7 @@ def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, w
     if out is None:
         out = torch.empty(image.shape, dtype=out_dtype or torch.float32, device=image.device)
     flags = (0 if quantise else FLAG_NO_QUANT) | (FLAG_WRITEBACK_SHIFT if writeback_shift else 0) | \
-        (0 if level_shift else FLAG_NO_SHIFT)
+        (0 if level_shift else FLAG_NO_SHIFT) | (FLAG_ROW_FIRST if row_first else 0)
     tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
     _check(load_library().hpdct_forward(ctypes.c_void_p(image.data_ptr()), _dtype_code(image),
                                         ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
@@ -217,7 +222,7 @@ def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, w
 
 
 def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, level_shift=True,
-            height=None, width=None, stream=None):
+            row_first=False, writeback_dequant=False, height=None, width=None, stream=None):
     """Fused inverse pass: T^T.(q*Q).T + 128 per tile.  out float32 (no clamp,
     as the reference) or uint8 (clamp + truncate, convertToUnsignedChar)."""
     torch = _torch()
@@ -226,7 +231,8 @@ def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, 
     h, w = _hw(coef, height, width)
     if out is None:
         out = torch.empty(coef.shape, dtype=out_dtype or torch.float32, device=coef.device)
-    flags = (0 if dequantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT)
+    flags = (0 if dequantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT) | \
+        (FLAG_ROW_FIRST if row_first else 0) | (FLAG_WRITEBACK_DEQUANT if writeback_dequant else 0)
     tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
     _check(load_library().hpdct_inverse(ctypes.c_void_p(coef.data_ptr()), _dtype_code(coef),
                                         ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
@@ -278,6 +284,21 @@ def idct_all_blocks_cuda(image_matrix, img_height: int, img_width: int, transfor
     f = getattr(load_library(), COMPAT_SYMBOLS["idct_all_blocks_cuda"])
     f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
       ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()))
+
+
+def dct_all_blocks(image_matrix, img_height: int, img_width: int, transform_matrix, result, handle=None) -> None:
+    """cublasDCTv2 surface (main_cublass_2.cu:197-252): row pass first, X-128
+    left in image_matrix; the cuBLAS handle is accepted and ignored."""
+    f = getattr(load_library(), COMPAT_SYMBOLS["dct_all_blocks"])
+    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
+      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()), handle)
+
+
+def idct_all_blocks(image_matrix, img_height: int, img_width: int, transform_matrix, result, handle=None) -> None:
+    """main_cublass_2.cu:257-311: q*Q left in image_matrix, D.T first."""
+    f = getattr(load_library(), COMPAT_SYMBOLS["idct_all_blocks"])
+    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
+      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()), handle)
 
 
 # ---------------------------------------------------------------------------

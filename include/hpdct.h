@@ -18,6 +18,8 @@
  *   hpdct_inverse          idct_all_blocks_cuda     main_newAppr.cu:293-332
  *                          (multiply_matrices -> cuda_matrix_idct ->
  *                          add_matrix_scalar fused into one pass)
+ *   hpdct_forward(..., HPDCT_FLAG_ROW_FIRST)  dct_all_blocks  main_cublass_2.cu:197-252
+ *   hpdct_inverse(..., HPDCT_FLAG_ROW_FIRST)  idct_all_blocks main_cublass_2.cu:257-311
  *   hpdct_set_quant_table  cudaMemcpyToSymbol(const_quant_matrix, ...)
  *                          main_newAppr.cu:19,70 (Q is library-owned here)
  *   hpdct_default_*        the Q and T tables of main_newAppr.cu:60-81
@@ -64,6 +66,11 @@ typedef enum hpdct_dtype {
                                            input buffer, as the reference's in-place sub_matrix_scalar
                                            does (main_newAppr.cu:273) */
 #define HPDCT_FLAG_NO_SHIFT 0x4u       /* skip the -128 / +128 level shift (diagnostics, round trips) */
+#define HPDCT_FLAG_ROW_FIRST 0x8u      /* fp32 -> fp32 only: cublasDCTv2 pass order (main_cublass_2.cu:228-235,
+                                          288-295): the row pass X.T^T (D.T) before the column pass */
+#define HPDCT_FLAG_WRITEBACK_DEQUANT 0x10u /* inverse, fp32 -> fp32 with dequantisation: also store q*Q back
+                                              into the coefficient buffer, as the cublasDCTv2 inverse's in-place
+                                              multiply_matrices does (main_cublass_2.cu:285) */
 
 /* Library / error information. */
 const char* hpdct_version(void);

@@ -5,6 +5,8 @@
  * bind (checked with g++ name mangling):
  *   _Z19dct_all_blocks_cudaPfiiPKfS_     dct_all_blocks_cuda
  *   _Z20idct_all_blocks_cudaPKfiiS0_Pf   idct_all_blocks_cuda
+ *   _Z14dct_all_blocksPfiiPKfS_P13cublasContext    dct_all_blocks   (cublasDCTv2)
+ *   _Z15idct_all_blocksPfiiPKfS_P13cublasContext   idct_all_blocks  (cublasDCTv2)
  *
  * Semantics kept from the reference (main_newAppr.cu:252-332):
  *   - all four pointers are DEVICE pointers owned by the caller; T is the
@@ -24,6 +26,16 @@
  *     EXIT_FAILURE instead of silently computing garbage;
  *   - one fused kernel per call, no per-call device allocation.
  * Set HPDCT_COMPAT_QUIET=1 in the environment to suppress the timing line.
+ *
+ * cublasDCTv2 surface (main_cublass_2.cu:36-37,197-311): same conventions,
+ * plus its pass order (row pass X.T^T first, inverse D.T first) and its
+ * in-place effects (X-128 left in the image, q*Q left in the coefficient
+ * buffer).  The cuBLAS handle is accepted and never dereferenced: the
+ * arithmetic runs in the library's own kernel.  Its summation order inside
+ * cuBLAS is not knowable here, so parity with a cuBLAS build is
+ * tolerance-only.  `struct cublasContext` is only the opaque tag
+ * cuBLAS's cublasHandle_t points to; it is named here so the mangled symbols
+ * match the reference's callers, nothing of cuBLAS is declared or used.
  */
 #ifndef HPDCT_COMPAT_H
 #define HPDCT_COMPAT_H
@@ -31,10 +43,16 @@
 #include "hpdct.h"
 
 #ifdef __cplusplus
+struct cublasContext;  // opaque handle tag (never dereferenced)
+
 void dct_all_blocks_cuda(float* image_matrix, const int img_height, const int img_width,
                          const float* transform_matrix, float* result);
 void idct_all_blocks_cuda(const float* image_matrix, const int img_height, const int img_width,
                           const float* transform_matrix, float* result);
+void dct_all_blocks(float* image_matrix, int img_height, int img_width, const float* transform_matrix, float* result,
+                    cublasContext* handle);
+void idct_all_blocks(float* image_matrix, int img_height, int img_width, const float* transform_matrix, float* result,
+                     cublasContext* handle);
 #endif
 
 #endif /* HPDCT_COMPAT_H */

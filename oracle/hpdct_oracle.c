@@ -153,7 +153,12 @@ enum {
     ORACLE_QUANT = 1,   /* forward: ÷Q + round; inverse: ×Q first          */
     ORACLE_NOFMA = 2,   /* diagnostic: separate multiply and add roundings */
     ORACLE_RECIP = 4,   /* diagnostic: C * (1/Q) instead of C / Q          */
-    ORACLE_NOSHIFT = 8  /* skip the -128 / +128 level shift                */
+    ORACLE_NOSHIFT = 8, /* skip the -128 / +128 level shift                */
+    ORACLE_ROWFIRST = 16 /* cublasDCTv2 pass order (main_cublass_2.cu:228-235,
+                            288-295): forward R = X.T^T then C = T.R; inverse
+                            R = D.T then C = T^T.R.  cuBLAS's own summation
+                            order is modelled as a sequential FMA chain over
+                            the 8 non-trivial k of each block (unpinned). */
 };
 
 static inline float mac(float a, float b, float s, int nofma) {
@@ -169,6 +174,24 @@ static inline float mac(float a, float b, float s, int nofma) {
 static void fdct_tile(const float x[8][8], const float* T, const float* Q, float c[8][8], int mode) {
     const int nofma = mode & ORACLE_NOFMA;
     float p[8][8];
+    if (mode & ORACLE_ROWFIRST) {
+        /* R[i][u] = sum_j X[i][j] T[u][j] (temp1 = X.Te^T), C[v][u] = sum_i T[v][i] R[i][u] */
+        float r[8][8];
+        for (int i = 0; i < 8; ++i)
+            for (int u = 0; u < 8; ++u) {
+                float s = 0.0f;
+                for (int j = 0; j < 8; ++j) s = mac(x[i][j], T[u * 8 + j], s, nofma);
+                r[i][u] = s;
+            }
+        for (int v = 0; v < 8; ++v)
+            for (int u = 0; u < 8; ++u) {
+                float s = 0.0f;
+                for (int i = 0; i < 8; ++i) s = mac(T[v * 8 + i], r[i][u], s, nofma);
+                if (mode & ORACLE_QUANT) s = roundf(s / Q[v * 8 + u]);
+                c[v][u] = s;
+            }
+        return;
+    }
     /* P[v][x] = sum_i T[v][i] * X[i][x]   (main_newAppr.cu:193-197) */
     for (int v = 0; v < 8; ++v)
         for (int col = 0; col < 8; ++col) {
@@ -204,6 +227,23 @@ static void idct_tile(const float d_in[8][8], const float* T, const float* Q, fl
     float d[8][8], p[8][8];
     for (int i = 0; i < 8; ++i)
         for (int j = 0; j < 8; ++j) d[i][j] = (mode & ORACLE_QUANT) ? d_in[i][j] * Q[i * 8 + j] : d_in[i][j];
+    if (mode & ORACLE_ROWFIRST) {
+        /* R[i][u] = sum_j D[i][j] T[j][u] (temp1 = D.Te), C[v][u] = sum_i T[i][v] R[i][u] */
+        float rr[8][8];
+        for (int i = 0; i < 8; ++i)
+            for (int u = 0; u < 8; ++u) {
+                float s = 0.0f;
+                for (int j = 0; j < 8; ++j) s = mac(d[i][j], T[j * 8 + u], s, nofma);
+                rr[i][u] = s;
+            }
+        for (int v = 0; v < 8; ++v)
+            for (int u = 0; u < 8; ++u) {
+                float s = 0.0f;
+                for (int i = 0; i < 8; ++i) s = mac(T[i * 8 + v], rr[i][u], s, nofma);
+                r[v][u] = (mode & ORACLE_NOSHIFT) ? s : s + 128.0f;
+            }
+        return;
+    }
     /* P[v][x] = sum_i T[i][v] * D[i][x]   (main_newAppr.cu:236-239) */
     for (int v = 0; v < 8; ++v)
         for (int col = 0; col < 8; ++col) {

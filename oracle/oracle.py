@@ -22,6 +22,7 @@ QUANT = 1
 NOFMA = 2
 RECIP = 4
 NOSHIFT = 8
+ROWFIRST = 16
 
 _lib = None
 _ref = None
@@ -107,14 +108,16 @@ def _tables(T, Q):
     return t, q
 
 
-def fdct(img: np.ndarray, T=None, Q=None, quant=True, nofma=False, recip=False, shift=True) -> np.ndarray:
+def fdct(img: np.ndarray, T=None, Q=None, quant=True, nofma=False, recip=False, shift=True,
+         row_first=False) -> np.ndarray:
     """Forward transform of a (H, W) uint8 or float32 image (not mutated)."""
     img = np.ascontiguousarray(img)
     h, w = img.shape[-2] if img.ndim > 1 else 1, img.shape[-1]
     h = img.size // w
     out = np.empty(img.shape, np.float32)
     t, q = _tables(T, Q)
-    mode = (QUANT if quant else 0) | (NOFMA if nofma else 0) | (RECIP if recip else 0) | (0 if shift else NOSHIFT)
+    mode = (QUANT if quant else 0) | (NOFMA if nofma else 0) | (RECIP if recip else 0) | (0 if shift else NOSHIFT) | \
+        (ROWFIRST if row_first else 0)
     fn = lib().oracle_fdct_u8 if img.dtype == np.uint8 else lib().oracle_fdct
     if img.dtype not in (np.uint8, np.float32):
         raise TypeError(img.dtype)
@@ -122,13 +125,13 @@ def fdct(img: np.ndarray, T=None, Q=None, quant=True, nofma=False, recip=False, 
     return out
 
 
-def idct(coef: np.ndarray, T=None, Q=None, dequant=True, nofma=False, shift=True) -> np.ndarray:
+def idct(coef: np.ndarray, T=None, Q=None, dequant=True, nofma=False, shift=True, row_first=False) -> np.ndarray:
     coef = np.ascontiguousarray(coef, dtype=np.float32)
     w = coef.shape[-1]
     h = coef.size // w
     out = np.empty(coef.shape, np.float32)
     t, q = _tables(T, Q)
-    mode = (QUANT if dequant else 0) | (NOFMA if nofma else 0) | (0 if shift else NOSHIFT)
+    mode = (QUANT if dequant else 0) | (NOFMA if nofma else 0) | (0 if shift else NOSHIFT) | (ROWFIRST if row_first else 0)
     lib().oracle_idct(_p(coef), h, w, None if t is None else _p(t), None if q is None else _p(q), _p(out), mode)
     return out
 

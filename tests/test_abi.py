@@ -61,6 +61,17 @@ def test_compat_mangling_matches_reference_signatures(tmp_path):
     out = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
     assert "_Z19dct_all_blocks_cudaPfiiPKfS_" in out
     assert "_Z20idct_all_blocks_cudaPKfiiS0_Pf" in out
+    # cublasDCTv2 (main_cublass_2.cu:36-37), with cuBLAS's handle typedef
+    src.write_text(
+        "typedef struct cublasContext *cublasHandle_t;\n"
+        "void dct_all_blocks(float *image_matrix, int img_height, int img_width, const float *transform_matrix,"
+        " float *result, cublasHandle_t handle) {}\n"
+        "void idct_all_blocks(float *image_matrix, int img_height, int img_width, const float *transform_matrix,"
+        " float *result, cublasHandle_t handle) {}\n")
+    subprocess.run(["g++", "-c", str(src), "-o", str(obj)], check=True)
+    out = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
+    assert "_Z14dct_all_blocksPfiiPKfS_P13cublasContext" in out
+    assert "_Z15idct_all_blocksPfiiPKfS_P13cublasContext" in out
 
 
 def test_kernels_are_gfx950_code_objects(hp):
@@ -125,6 +136,13 @@ def test_bad_arguments_rejected(hp):
     assert L.hpdct_inverse(a, hp.U8, b, hp.F32, 8, 8, None, 0, None) == 2
     assert L.hpdct_inverse(a, hp.F32, b, hp.I8, 8, 8, None, 0, None) == 2
     assert L.hpdct_inverse(a, hp.F32, b, hp.F32, 8, 8, None, hp.FLAG_WRITEBACK_SHIFT, None) == 2
+    # cublasDCTv2 options are fp32 -> fp32 only; the dequant write-back needs dequantisation
+    assert L.hpdct_forward(a, hp.U8, b, hp.F32, 8, 8, None, hp.FLAG_ROW_FIRST, None) == 2
+    assert L.hpdct_forward(a, hp.F32, b, hp.F32, 8, 8, None, hp.FLAG_WRITEBACK_DEQUANT, None) == 2
+    assert L.hpdct_inverse(a, hp.I8, b, hp.F32, 8, 8, None, hp.FLAG_ROW_FIRST, None) == 2
+    assert L.hpdct_inverse(a, hp.F32, b, hp.U8, 8, 8, None, hp.FLAG_WRITEBACK_DEQUANT, None) == 2
+    assert L.hpdct_inverse(a, hp.F32, b, hp.F32, 8, 8, None,
+                           hp.FLAG_WRITEBACK_DEQUANT | hp.FLAG_NO_QUANT, None) == 2
     # int8 output refused when the table can overflow int8
     hp.set_quant_table(np.ones(64, np.float32))
     try:

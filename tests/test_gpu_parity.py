@@ -292,6 +292,60 @@ def test_compat_entry_points():
     assert "NOT REACHED" not in p.stdout and "AssertionError" not in p.stderr
 
 
+# --------------------------------------------------------------------- cublasDCTv2 order
+def test_row_first_paths(hp, oracle, dev, c1):
+    import torch
+    img = c1.astype(np.float32)
+    T = to_dev(hp.default_transform(), dev)
+    for tr in (None, T):
+        q = to_host(hp.forward(to_dev(img, dev), row_first=True, transform=tr))
+        assert bits_equal(q, oracle.fdct(c1, row_first=True))
+        c = to_host(hp.forward(to_dev(img, dev), row_first=True, quantise=False, transform=tr))
+        assert bits_equal(c, oracle.fdct(c1, row_first=True, quant=False))
+        qd = to_dev(q, dev)
+        r = to_host(hp.inverse(qd, row_first=True, writeback_dequant=True, transform=tr))
+        assert bits_equal(r, oracle.idct(q, row_first=True))
+        assert bits_equal(to_host(qd), q * oracle.default_quant()[np.arange(256) % 8][:, np.arange(256) % 8])
+    # the HpApprDCT inverse with the dequant write-back
+    q = oracle.fdct(c1)
+    qd = to_dev(q, dev)
+    r = to_host(hp.inverse(qd, writeback_dequant=True))
+    assert bits_equal(r, oracle.idct(q))
+    assert not bits_equal(to_host(qd), q)
+
+
+_CUBLAS_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [{pkg!r}, {orc!r}]
+import hpdct, oracle
+dev = torch.device("cuda:0")
+c1 = oracle.rand_u8(256 * 256, 42).reshape(256, 256)
+img = torch.from_numpy(c1.astype(np.float32)).to(dev)
+T = torch.from_numpy(hpdct.default_transform()).to(dev)
+res = torch.empty_like(img)
+hpdct.dct_all_blocks(img, 256, 256, T, res)
+q = oracle.fdct(c1, row_first=True)
+assert np.array_equal(res.cpu().numpy().view(np.uint32), q.view(np.uint32)), "forward"
+assert np.array_equal(img.cpu().numpy(), c1.astype(np.float32) - 128.0), "in-place X-128"
+out = torch.empty_like(img)
+hpdct.idct_all_blocks(res, 256, 256, T, out)
+assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.idct(q, row_first=True).view(np.uint32)), "inverse"
+Q = np.tile(oracle.default_quant(), (32, 32))
+assert np.array_equal(res.cpu().numpy(), q * Q), "in-place q*Q"
+print("CUBLAS-SURFACE-OK")
+"""
+
+
+def test_cublas_surface_entry_points():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _CUBLAS_SCRIPT.format(pkg=os.path.join(root, "cuda-dct-idct_amd"), orc=os.path.join(root, "oracle"))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert "CUBLAS-SURFACE-OK" in p.stdout and "DCT (256,256): " in p.stdout and "IDCT (256,256): " in p.stdout
+
+
 # --------------------------------------------------------------------- generator
 @pytest.mark.parametrize("n,first", [(4096, 0), (1000, 12345), (17, 3)])
 def test_fill_hash_matches_oracle(hp, oracle, dev, n, first):

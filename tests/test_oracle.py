@@ -191,3 +191,23 @@ def test_conversions_match_reference_live(oracle):
     uc = np.empty(xs.size, np.uint8)
     R._Z21convertToUnsignedCharPKfPhm(xs.ctypes.data, uc.ctypes.data, xs.size)
     assert np.array_equal(oracle.to_u8(xs), uc)
+
+
+# ---------------------------------------------------------------- cublasDCTv2 order
+def test_row_first_order(oracle):
+    """main_cublass_2.cu:228-235/288-295: the same transform with the row pass
+    first.  Unquantised it agrees with the HpApprDCT order to fp32 rounding;
+    quantised, values near a rounding boundary may move by one step."""
+    img = oracle.rand_u8(256 * 256).reshape(256, 256)
+    a = oracle.fdct(img, quant=False)
+    b = oracle.fdct(img, quant=False, row_first=True)
+    assert 0 < np.abs(a - b).max() < 1e-4
+    qa, qb = oracle.fdct(img), oracle.fdct(img, row_first=True)
+    assert np.abs(qa - qb).max() <= 1.0 and 0 < int((qa != qb).sum()) < 200
+    rt = oracle.idct(b, dequant=False, row_first=True)
+    assert np.abs(rt - img).max() < 1e-4
+    # separable transform of an impulse: identical in both orders
+    imp = np.full((8, 8), 128, np.uint8)
+    imp[2, 5] = 200
+    assert np.array_equal(oracle.fdct(imp, quant=False), oracle.fdct(imp, quant=False, row_first=True)) or \
+        np.abs(oracle.fdct(imp, quant=False) - oracle.fdct(imp, quant=False, row_first=True)).max() < 1e-5
