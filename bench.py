@@ -217,6 +217,21 @@ def main():
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
         extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world)
+        # the reference's own two GPU decompositions of the same arithmetic, on
+        # this GPU (include/hpdct_baseline.h): 3 launches per frame, fp32 in/out
+        T = torch.from_numpy(hpdct.default_transform()).to(dev)
+        bimg = imgs[0].float()
+        btmp = torch.empty_like(bimg)
+        bres = torch.empty_like(bimg)
+        for kind in ("reference_3pass", "fastappr_3pass"):
+            calls = [lambda k=kind: hpdct.baseline_forward(k, bimg, btmp, bres, T, stream=stream)]
+            bsteps = max(10, steps // 4)
+            rms, k, _ = timed_loop(calls, bsteps, 3)
+            extras["baseline_" + kind] = {
+                "ms_per_frame": round(rms / bsteps, 4), "gpx_s": round(px / (rms / bsteps * 1e-3) / 1e9, 2),
+                "note": "the reference's 3-launch structure re-expressed in HIP on this MI355X (fp32 in/out, "
+                        "X-128 in place); same arithmetic, bit-identical output"}
+        del bimg, btmp, bres
         # C3 round trip quality on the reference's frame
         hpdct.forward(imgs[0], outs[0])
         r = hpdct.inverse(outs[0], rec[0])

@@ -48,7 +48,9 @@ C_SYMBOLS = [
     "hpdct_forward", "hpdct_inverse",
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
+    "hpdct_baseline_forward",
 ]
+BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
 COMPAT_SYMBOLS = {
     "dct_all_blocks_cuda": "_Z19dct_all_blocks_cudaPfiiPKfS_",
     "idct_all_blocks_cuda": "_Z20idct_all_blocks_cudaPKfiiS0_Pf",
@@ -117,6 +119,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_u8_to_f32.restype = None
     lib.hpdct_f32_to_u8.argtypes = [vp, vp, i64]
     lib.hpdct_f32_to_u8.restype = None
+    lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
+    lib.hpdct_baseline_forward.restype = ctypes.c_int
     for name, mangled in COMPAT_SYMBOLS.items():
         f = getattr(lib, mangled)
         f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp] + ([vp] if not name.endswith("_cuda") else [])
@@ -259,6 +263,18 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
         if st:
             _check(st)
     return call
+
+
+def baseline_forward(kind: str, image, tmp, result, transform, stream=None) -> None:
+    """A/B baselines (include/hpdct_baseline.h): the reference's 3-launch
+    HpApprDCT structure or the fastApprDCT row-per-thread structure on the GPU.
+    Mutates `image` to X-128 like the reference."""
+    h, w = _hw(image, None, None)
+    st = load_library().hpdct_baseline_forward(BASELINES[kind], ctypes.c_void_p(image.data_ptr()),
+                                               ctypes.c_void_p(tmp.data_ptr()), ctypes.c_void_p(result.data_ptr()),
+                                               h, w, ctypes.c_void_p(transform.data_ptr()), _stream_ptr(stream))
+    if st:
+        raise HpdctError(st, "baseline launch failed")
 
 
 def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):

@@ -346,6 +346,21 @@ def test_cublas_surface_entry_points():
     assert "CUBLAS-SURFACE-OK" in p.stdout and "DCT (256,256): " in p.stdout and "IDCT (256,256): " in p.stdout
 
 
+# --------------------------------------------------------------------- A/B baselines
+@pytest.mark.parametrize("kind", ["reference_3pass", "fastappr_3pass"])
+@pytest.mark.parametrize("h,w", [(256, 256), (24, 72), (64, 8)])
+def test_baselines_bitexact(hp, oracle, dev, kind, h, w):
+    import torch
+    img8 = np.random.default_rng(h + w).integers(0, 256, (h, w), dtype=np.uint8)
+    img = to_dev(img8.astype(np.float32), dev)
+    tmp = torch.empty_like(img)
+    res = torch.empty_like(img)
+    T = to_dev(hp.default_transform(), dev)
+    hp.baseline_forward(kind, img, tmp, res, T)
+    assert bits_equal(to_host(res), oracle.fdct(img8))
+    assert np.array_equal(to_host(img), img8.astype(np.float32) - 128.0)
+
+
 # --------------------------------------------------------------------- generator
 @pytest.mark.parametrize("n,first", [(4096, 0), (1000, 12345), (17, 3)])
 def test_fill_hash_matches_oracle(hp, oracle, dev, n, first):

@@ -74,6 +74,17 @@ __global__ __launch_bounds__(256) void mix_w16(const uint4* __restrict__ in, flo
     }
 }
 
+// fp32 -> fp32 (4 B in + 4 B out per px), 16 B per lane each way, grid-stride
+template <bool kNT>
+__global__ __launch_bounds__(256) void copy_f32(const float4* __restrict__ in, float4* __restrict__ out, uint64_t n4) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n4; i += stride) {
+        float4 v = in[i];
+        v.x -= 128.f; v.y -= 128.f; v.z -= 128.f; v.w -= 128.f;
+        st4<kNT>(&out[i], v);
+    }
+}
+
 template <bool kNT>
 __global__ __launch_bounds__(256) void write_only(float4* __restrict__ out, uint64_t n4) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -200,6 +211,17 @@ int main(int argc, char** argv) {
                                                 (float4*)out[s], n16);
                          }});
     }
+    for (int gm : {2, 4, 8, 16}) {
+        const unsigned grid = cus * gm;
+        cases.push_back({"copy_f32 plain g" + std::to_string(gm), 8.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(copy_f32<false>, dim3(grid), dim3(256), 0, 0,
+                                                (const float4*)out[(s + 1) % nsets], (float4*)out[s], n4);
+                         }});
+        cases.push_back({"copy_f32 nt    g" + std::to_string(gm), 8.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(copy_f32<true>, dim3(grid), dim3(256), 0, 0,
+                                                (const float4*)out[(s + 1) % nsets], (float4*)out[s], n4);
+                         }});
+    }
     const uint32_t ntiles = px / 64, tiles_x = n / 8;
     cases.push_back({"tile_mix plain", 5.0 * px, [=](int s) {
                          hipLaunchKernelGGL(tile_mix<false>, dim3((ntiles + 255) / 256), dim3(256), 0, 0, in[s],
@@ -227,6 +249,14 @@ int main(int argc, char** argv) {
                      }});
     cases.push_back({"hipMemsetD32 4B/px", 4.0 * px, [=](int s) { CK(hipMemsetD32Async((hipDeviceptr_t)out[s], 7, px, 0)); }});
 
+    if (argc > 3 && strcmp(argv[3], "f32") == 0) {
+        std::vector<Case> keep;
+        for (auto& c : cases)
+            if (c.name.find("copy_f32") != std::string::npos || c.name.find("D2D") != std::string::npos ||
+                c.name.find("mix_w4 nt    g4") != std::string::npos)
+                keep.push_back(c);
+        cases.swap(keep);
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
