@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--c4-size", type=int, default=16384)
+    ap.add_argument("--c5-size", type=int, default=4096)
+    ap.add_argument("--c5-frames", type=int, default=512)
     return ap.parse_args()
 
 
@@ -243,6 +245,7 @@ def main():
         del f32_in, i8, rec
         torch.cuda.empty_cache()
         extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks)
+        extras["c5"] = _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks)
         result["extras"] = extras
 
     # ------------------------------------------------------------ CPU baseline
@@ -341,6 +344,36 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     del x, y
     torch.cuda.empty_cache()
     return out
+
+
+def _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks):
+    """C5: a batch of independent 4096^2 frames streamed from pinned host memory
+    through H2D -> forward kernel -> D2H, overlapped over HIP streams
+    (hpdct_stream_forward); replicas only: every rank takes its share of the
+    batch, no collective.  Host frames: a pool of 8 pinned frames (srand(seed),
+    seeds 42..49) cycled over the batch."""
+    n = args.c5_size
+    frames_total = args.c5_frames
+    mine = frames_total // world + (1 if rank < frames_total % world else 0)
+    pool_in = []
+    for k in range(8):
+        t = torch.empty((n, n), dtype=torch.uint8).pin_memory()
+        t.copy_(torch.from_numpy(hpdct.fill_rand_u8(n * n, 42 + k).reshape(n, n)))
+        pool_in.append(t)
+    res = {"frame": [n, n], "frames_total": frames_total, "frames_per_rank": mine}
+    for out_dtype, name, obytes in ((torch.float32, "f32", 4), (torch.int8, "i8", 1)):
+        pool_out = [torch.empty((n, n), dtype=out_dtype).pin_memory() for _ in range(8)]
+        frames = [pool_in[i % 8] for i in range(mine)]
+        outs = [pool_out[i % 8] for i in range(mine)]
+        hpdct.stream_forward(frames[:8], outs[:8], nstreams=3)  # warm-up
+        barrier()
+        ms = max_over_ranks(hpdct.stream_forward(frames, outs, nstreams=3))
+        moved = mine * n * n * (1 + obytes)
+        res[name] = {"ms": round(ms, 2), "frames_per_s_total": round(frames_total / (ms * 1e-3), 1),
+                     "gpx_s_total": round(frames_total * n * n / (ms * 1e-3) / 1e9, 2),
+                     "pcie_GBs_per_rank": round(moved / (ms * 1e-3) / 1e9, 1)}
+        del pool_out, outs
+    return res
 
 
 def _cpu_baseline(n):

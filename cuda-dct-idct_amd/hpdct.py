@@ -48,7 +48,7 @@ C_SYMBOLS = [
     "hpdct_forward", "hpdct_inverse",
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
-    "hpdct_baseline_forward",
+    "hpdct_baseline_forward", "hpdct_stream_forward",
 ]
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
 COMPAT_SYMBOLS = {
@@ -119,6 +119,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_u8_to_f32.restype = None
     lib.hpdct_f32_to_u8.argtypes = [vp, vp, i64]
     lib.hpdct_f32_to_u8.restype = None
+    lib.hpdct_stream_forward.argtypes = [vp, vp, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp]
+    lib.hpdct_stream_forward.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
     lib.hpdct_baseline_forward.restype = ctypes.c_int
     for name, mangled in COMPAT_SYMBOLS.items():
@@ -275,6 +277,23 @@ def baseline_forward(kind: str, image, tmp, result, transform, stream=None) -> N
                                                h, w, ctypes.c_void_p(transform.data_ptr()), _stream_ptr(stream))
     if st:
         raise HpdctError(st, "baseline launch failed")
+
+
+def stream_forward(frames, outs, nstreams: int = 3) -> float:
+    """Config C5: host-resident (pinned) uint8 frames -> host coefficient planes
+    with H2D / kernel / D2H overlapped over `nstreams` HIP streams.  `frames`
+    and `outs` are equal-length lists of CPU tensors (entries may repeat).
+    Returns the device-timed milliseconds of the whole batch."""
+    n = len(frames)
+    if n != len(outs) or n == 0:
+        raise HpdctError(1, "frames and outs must be non-empty lists of equal length")
+    h, w = _hw(frames[0], None, None)
+    fp = (ctypes.c_void_p * n)(*[f.data_ptr() for f in frames])
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    ms = ctypes.c_float()
+    _check(load_library().hpdct_stream_forward(fp, op, n, h, w, _dtype_code(outs[0]), int(nstreams),
+                                               ctypes.byref(ms)))
+    return ms.value
 
 
 def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):

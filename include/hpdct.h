@@ -122,6 +122,19 @@ hpdct_status hpdct_forward_u8_i8(const uint8_t* d_image, int8_t* d_coef, int64_t
 hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t height, int64_t width,
                                    void* stream);
 
+/* Host-resident batch (BASELINE config C5): frame f (height x width uint8 at
+ * h_frames[f]) -> coefficients at h_coef[f] (out_type HPDCT_F32 or HPDCT_I8),
+ * pipelined over nstreams (1..16) HIP streams, each with one device input and
+ * one output buffer: H2D copy, fused forward kernel and D2H copy of different
+ * frames overlap.  Pointers may repeat (a pool cycled over the batch).  Host
+ * buffers should be pinned for the copies to overlap.  Synchronous: returns
+ * when every coefficient plane is in host memory; *elapsed_ms (may be NULL)
+ * receives the device-timed span of the batch.  Replaces the reference's
+ * one-image blocking H2D/compute/D2H sequence (benchmark_newAppr.cu:88-109). */
+hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
+                                  int64_t height, int64_t width, hpdct_dtype out_type, int nstreams,
+                                  float* elapsed_ms);
+
 /* Synthetic frames generated on the device (BASELINE config C4): pixel
  * i of the frame = splitmix64(seed, first_index + i) & 255 (the oracle's
  * oracle_fill_hash_u8 restates it). */

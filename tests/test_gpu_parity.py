@@ -346,6 +346,26 @@ def test_cublas_surface_entry_points():
     assert "CUBLAS-SURFACE-OK" in p.stdout and "DCT (256,256): " in p.stdout and "IDCT (256,256): " in p.stdout
 
 
+# --------------------------------------------------------------------- C5 host streaming
+@pytest.mark.parametrize("nstreams", [1, 3])
+def test_stream_forward_host_batch(hp, oracle, dev, nstreams):
+    import torch
+    h, w = 64, 136
+    pool = [torch.from_numpy(oracle.rand_u8(h * w, 42 + k).reshape(h, w)).pin_memory() for k in range(3)]
+    frames = [pool[i % 3] for i in range(10)]
+    outs = [torch.full((h, w), -7.0).pin_memory() for _ in range(10)]
+    ms = hp.stream_forward(frames, outs, nstreams=nstreams)
+    assert ms > 0
+    for f, o in zip(frames, outs):
+        assert bits_equal(o.numpy(), oracle.fdct(f.numpy()))
+    outs8 = [torch.zeros((h, w), dtype=torch.int8).pin_memory() for _ in range(4)]
+    hp.stream_forward(frames[:4], outs8, nstreams=nstreams)
+    for f, o in zip(frames[:4], outs8):
+        assert np.array_equal(o.numpy(), oracle.fdct(f.numpy()).astype(np.int8))
+    with pytest.raises(hp.HpdctError):
+        hp.stream_forward(frames[:2], outs[:1])
+
+
 # --------------------------------------------------------------------- A/B baselines
 @pytest.mark.parametrize("kind", ["reference_3pass", "fastappr_3pass"])
 @pytest.mark.parametrize("h,w", [(256, 256), (24, 72), (64, 8)])
