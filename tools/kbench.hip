@@ -56,6 +56,82 @@ __global__ __launch_bounds__(256) void copy_linear(const uint32_t* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------
+// A/B: the north_star's sketch -- one wavefront per 8x8 tile, lane (r, c) =
+// pixel, row/column passes through wavefront shuffles (ds_bpermute), u8 rows
+// loaded wide and staged in LDS, T rows per lane in VGPRs (the FMA constants
+// differ per lane, so no zero-term skipping), outputs staged in LDS and
+// written as 1 KiB-contiguous non-temporal stores.  Each wave walks strips of
+// 8 horizontally adjacent tiles (64 px x 8 rows).  Same arithmetic: the output
+// is checked bit-for-bit against the product kernel.
+template <bool kUnroll>
+__global__ __launch_bounds__(256) void wave_per_tile_kernel(const uint8_t* __restrict__ img, float* __restrict__ out,
+                                                            TileGrid g, QParams qp) {
+    __shared__ uint2 sin[4][64];        // per wave: 8 rows x 8 tiles x 8 B
+    __shared__ float sout[4][8 * 64];   // per wave: 8 rows x 64 floats
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t r = lane >> 3, c = lane & 7u;
+    float trow[8], tcol[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        trow[i] = kBuiltinT.v[r * 8 + i];  // column pass: T[r][i]
+        tcol[i] = kBuiltinT.v[c * 8 + i];  // row pass: T[c][i]
+    }
+    const float qv = qp.q.v[r * 8 + c], rv = qp.r.v[r * 8 + c];
+    const uint32_t strips = g.ntiles / 8u;  // tiles_x multiple of 8 assumed (checked by the launcher)
+    const uint32_t strip = (blockIdx.x * 4u + w);
+    if (strip >= strips) return;
+    const uint32_t t0 = strip * 8u;
+    const uint32_t ty = t0 / g.tiles_x, tx = t0 - ty * g.tiles_x;
+    const uint64_t base = (uint64_t)ty * 8u * g.width + (uint64_t)tx * 8u;
+    // lane l loads tile (l & 7), row (l >> 3): 8 rows x 64 contiguous bytes
+    sin[w][r * 8 + c] = *reinterpret_cast<const uint2*>(img + base + r * g.width + 8u * c);
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(sin[w]);
+    auto tile = [&](int k) {
+        const float x = (float)sb[r * 64 + 8 * k + c] - 128.0f;
+        float p = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float xi = __int_as_float(__builtin_amdgcn_ds_bpermute((int)((i * 8 + c) << 2), __float_as_int(x)));
+            p = __builtin_fmaf(trow[i], xi, p);
+        }
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute((int)((r * 8 + i) << 2), __float_as_int(p)));
+            s = __builtin_fmaf(pi, tcol[i], s);
+        }
+        sout[w][r * 64 + 8 * k + c] = quantise<kVarFastDiv>(s, qv, rv);  // the product's verified quotient
+    };
+    if constexpr (kUnroll) {
+        unroll<8>([&](auto k) { tile(k); });
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < 8; ++k) tile(k);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // 8 rows x 256 B: two rows per 1 KiB... each lane stores float4 j of row (j / 16)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t j = h * 64u + lane;   // float4 index in the 8 x 16 strip
+        const uint32_t row = j >> 4, col4 = j & 15u;
+        const float4 v = reinterpret_cast<const float4*>(sout[w])[row * 16 + col4];
+        float4* dst = reinterpret_cast<float4*>(out + base + row * g.width) + col4;
+        __builtin_nontemporal_store(v.x, &dst->x);
+        __builtin_nontemporal_store(v.y, &dst->y);
+        __builtin_nontemporal_store(v.z, &dst->z);
+        __builtin_nontemporal_store(v.w, &dst->w);
+    }
+}
+
+template <bool kUnroll>
+void launch_wave_per_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                          hipStream_t s) {
+    const uint32_t strips = g.ntiles / 8u;
+    hipLaunchKernelGGL(wave_per_tile_kernel<kUnroll>, dim3((strips + 3) / 4), dim3(256), 0, s, in, out, g, qp);
+}
+
 struct Variant {
     std::string name;
     void (*launch)(const uint8_t*, float*, const TileGrid&, const QParams&, uint32_t cus, hipStream_t);
@@ -145,15 +221,10 @@ int main(int argc, char** argv) {
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
         {"product (b512+lds+nt+fast)", launch_var<B | W512>},
+        {"north_star: wave per tile", launch_wave_per_tile<false>},
+        {"north_star: wave per tile, 8 tiles unrolled", launch_wave_per_tile<true>},
     };
-    std::vector<Variant> other = {
-        {"fwd f32->f32 lds+nt b512 (8B/px)", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32->f32 +ldsload", launch_fwd_any<float, float, L | N | W512 | LL>, true},
-        {"inv f32->f32 lds+nt b512 (8B/px)", launch_inv_any<float, float, L | N | W512>, true},
-        {"inv f32->f32 +ldsload", launch_inv_any<float, float, L | N | W512 | LL>, true},
-        {"fwd f32->f32 plain b256", launch_fwd_any<float, float, 0>, true},
-        {"fwd f32->f32 nt-only b512", launch_fwd_any<float, float, N | W512>, true},
-    };
+    std::vector<Variant> other = {};
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
     launch_var<0>(in[0], out[0], g, qp, cus, 0);
