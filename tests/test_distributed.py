@@ -48,7 +48,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, height, width, result_path):
+def _worker(rank, world, port, height, width, result_path, wire_int8=False):
     import torch
     import torch.distributed as dist
     import oracle
@@ -62,10 +62,15 @@ def _worker(rank, world, port, height, width, result_path):
         # same stateless generator the bench uses on the device (C4)
         slab = oracle.hash_u8(rows * width, seed=42, first_index=r0 * width).reshape(rows, width)
         coef = torch.from_numpy(oracle.fdct(slab))
+        if wire_int8:  # the C4 int8 wire format: |q| <= 98, decoded to fp32 on the root
+            coef = coef.to(torch.int8)
         full = gather_slabs(coef, height, width, root=0)
         if rank == 0:
             ref = oracle.fdct(oracle.hash_u8(height * width, seed=42).reshape(height, width))
-            ok = np.array_equal(full.numpy().view(np.uint32), ref.view(np.uint32))
+            if wire_int8:
+                ok = np.array_equal(full.float().numpy(), ref)  # by value: the wire drops the sign of -0.0
+            else:
+                ok = np.array_equal(full.numpy().view(np.uint32), ref.view(np.uint32))
             with open(result_path, "w") as fh:
                 fh.write("ok" if ok else "mismatch")
         else:
@@ -74,9 +79,10 @@ def _worker(rank, world, port, height, width, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,height,width", [(2, 64, 96), (2, 72, 40), (3, 80, 64)])
-def test_sharded_gather_equals_unsharded(tmp_path, world, height, width):
+@pytest.mark.parametrize("world,height,width,wire", [(2, 64, 96, False), (2, 72, 40, False), (3, 80, 64, False),
+                                                     (2, 64, 96, True), (3, 72, 16, True)])
+def test_sharded_gather_equals_unsharded(tmp_path, world, height, width, wire):
     import torch.multiprocessing as mp
     result = tmp_path / "result.txt"
-    mp.spawn(_worker, args=(world, _free_port(), height, width, str(result)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), height, width, str(result), wire), nprocs=world, join=True)
     assert result.read_text() == "ok"
