@@ -44,6 +44,9 @@ enum : unsigned {
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
+    kVarNTLoad = 1u << 16,    // non-temporal loads of the 8-bit input planes
+    kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
+                              // coefficient converted straight into its byte (SDWA dst_sel, one op)
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
@@ -81,6 +84,36 @@ __device__ __forceinline__ uint32_t pack_u8x4(float a, float b, float c, float d
 // exhaustively by tests/tools/verify_round3.c (tests/test_tools.py).
 __device__ __forceinline__ float round_half_away(float x) {
     return __builtin_truncf(x + __builtin_copysignf(0.49999997f, x));
+}
+
+// the quotient C / Q (IEEE, or the verified 3-op form)
+template <unsigned kVar>
+__device__ __forceinline__ float quotient(float c, float q, float r) {
+    if constexpr (kVar & kVarFastDiv) {
+        const float q0 = c * r;
+        const float e = __builtin_fmaf(-q0, q, c);
+        return __builtin_fmaf(e, r, q0);
+    } else {
+        (void)r;
+        return c / q;
+    }
+}
+
+// int8 coefficients: round-half-away(d) = trunc(d + copysign(0.49999997, d))
+// and v_cvt_i32_f32 truncates, so the trunc is folded into the conversion;
+// each conversion writes its byte of the packed dword directly (SDWA dst_sel).
+__device__ __forceinline__ uint32_t pack_q_i8x4(float a, float b, float c, float d) {
+    auto biased = [](float x) { return x + __builtin_copysignf(0.49999997f, x); };
+    uint32_t w;
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD"
+                 : "=v"(w) : "v"(biased(a)));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(biased(b)));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(biased(c)));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(biased(d)));
+    return w;
 }
 
 // divide_matrices (utils_kernels.cu:42): round(C / Q)
@@ -122,6 +155,13 @@ struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
     uint2 r[8];
     __device__ __forceinline__ void load(const uint8_t* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
+    }
+    __device__ __forceinline__ void load_nt(const uint8_t* __restrict__ p, uint64_t width) {
+        unroll<8>([&](auto i) {
+            const uint2* q = reinterpret_cast<const uint2*>(p + i * width);
+            r[i].x = __builtin_nontemporal_load(&q->x);
+            r[i].y = __builtin_nontemporal_load(&q->y);
+        });
     }
     __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
         unroll<8>([&](auto i) {
@@ -291,6 +331,8 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
             } else {
                 raw.load(src + p.base, g.width);
             }
+        } else if constexpr ((kVar & kVarNTLoad) != 0 && std::is_same_v<TIn, uint8_t>) {
+            raw.load_nt(src + p.base, g.width);
         } else {
             raw.load(src + p.base, g.width);
         }
@@ -387,6 +429,12 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
             unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
         }
         auto emit = [&](auto v, float (&c)[8]) {
+            if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
+                unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+                const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
+                st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
+                return;
+            }
             if constexpr (kQuant) {
                 unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
             }
@@ -503,7 +551,8 @@ inline uint32_t device_cus() {
 // All product kernels use 512-thread workgroups (2u << 12: measured 1-3 %
 // faster than 256 on every kernel of the path, tools/kbench.hip).
 template <typename TIn, typename TOut>
-constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u);
+constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
+                              (std::is_same_v<TOut, int8_t> ? kVarI8Pack : 0u);
 
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev, const QParams& q,

@@ -218,13 +218,18 @@ int main(int argc, char** argv) {
     constexpr unsigned F = kVarFastDiv, X = kVarXorCvt, L = kVarLdsStore, N = kVarNT, P = kVarPersist;
     constexpr unsigned B = L | N | F, R = kVarRowMajor, S = kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
     constexpr unsigned LL = kVarLdsLoad;
+    constexpr unsigned NL = kVarNTLoad, IP = kVarI8Pack;
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
         {"product (b512+lds+nt+fast)", launch_var<B | W512>},
-        {"north_star: wave per tile", launch_wave_per_tile<false>},
-        {"north_star: wave per tile, 8 tiles unrolled", launch_wave_per_tile<true>},
+        {"product + nt loads", launch_var<B | W512 | NL>},
     };
-    std::vector<Variant> other = {};
+    std::vector<Variant> other = {
+        {"fwd u8->i8 +i8pack", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 +i8pack+xor", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP | X>},
+        {"fwd u8->i8 +i8pack no-nt", launch_fwd_any<uint8_t, int8_t, F | W512 | IP>},
+        {"fwd u8->i8 +i8pack b256", launch_fwd_any<uint8_t, int8_t, F | N | IP>},
+    };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
     launch_var<0>(in[0], out[0], g, qp, cus, 0);
@@ -249,7 +254,8 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> A(px * 4), Bv(px * 4);
         CK(hipMemcpy(A.data(), out[2], px * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(Bv.data(), out[3], px * 4, hipMemcpyDeviceToHost));
-        const size_t nb = other[v].name.find("->u8") != std::string::npos ? px : px * 4;
+        const size_t nb = (other[v].name.find("->u8") != std::string::npos ||
+                           other[v].name.find("->i8") != std::string::npos) ? px : px * 4;
         const bool ok = memcmp(A.data(), Bv.data(), nb) == 0;
         printf("check %-32s == %-24s %s\n", other[v + 1].name.c_str(), other[v].name.c_str(),
                ok ? "bit-exact" : "MISMATCH");
