@@ -125,6 +125,28 @@ def fdct(img: np.ndarray, T=None, Q=None, quant=True, nofma=False, recip=False, 
     return out
 
 
+def fdct_threads(img: np.ndarray, threads: int) -> np.ndarray:
+    """fdct (default tables, quantised) of a (H, W) uint8 image split into
+    `threads` bands of whole tile rows, one ctypes call per band on a thread
+    pool (ctypes drops the GIL): the all-cores CPU baseline.
+    Tiles are independent, so the result equals fdct(img) bit for bit."""
+    from concurrent.futures import ThreadPoolExecutor
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.empty(img.shape, np.float32)
+    trows = h // 8
+    cuts = [8 * (trows * k // threads) for k in range(threads + 1)]
+
+    def band(k):
+        r0, r1 = cuts[k], cuts[k + 1]
+        if r1 > r0:
+            lib().oracle_fdct_u8(_p(img[r0:r1]), r1 - r0, w, None, None, _p(out[r0:r1]), QUANT)
+
+    with ThreadPoolExecutor(max_workers=threads) as pool:
+        list(pool.map(band, range(threads)))
+    return out
+
+
 def idct(coef: np.ndarray, T=None, Q=None, dequant=True, nofma=False, shift=True, row_first=False) -> np.ndarray:
     coef = np.ascontiguousarray(coef, dtype=np.float32)
     w = coef.shape[-1]

@@ -211,3 +211,13 @@ def test_row_first_order(oracle):
     imp[2, 5] = 200
     assert np.array_equal(oracle.fdct(imp, quant=False), oracle.fdct(imp, quant=False, row_first=True)) or \
         np.abs(oracle.fdct(imp, quant=False) - oracle.fdct(imp, quant=False, row_first=True)).max() < 1e-5
+
+
+@pytest.mark.parametrize("h,w,threads", [(64, 96, 3), (8, 40, 4), (256, 256, 16)])
+def test_fdct_threads_equals_fdct(oracle, h, w, threads):
+    """The all-cores CPU baseline (bench.py cpu_baseline.all_cores) bands the
+    frame by tile rows; tiles are independent, so it is bit-identical."""
+    img = oracle.rand_u8(h * w, 7).reshape(h, w)
+    a = oracle.fdct_threads(img, threads)
+    b = oracle.fdct(img)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
