@@ -45,6 +45,18 @@ constexpr float kDefaultT[64] = {TA, TA,  TA,  TA,  TA,  TA,  TA,  TA,  TH, TH, 
 #undef TC
 #undef TD
 
+// hpdct_mapping in force: -1 = not yet read from HPDCT_MAPPING.
+std::atomic<int> g_mapping{-1};
+
+int mapping_from_env() {
+    const char* e = getenv("HPDCT_MAPPING");
+    if (!e || !*e || strcmp(e, "auto") == 0) return HPDCT_MAPPING_AUTO;
+    if (strcmp(e, "tile") == 0) return HPDCT_MAPPING_TILE;
+    if (strcmp(e, "octet") == 0) return HPDCT_MAPPING_OCTET;
+    fprintf(stderr, "hpdct: ignoring HPDCT_MAPPING=%s (expected auto, tile or octet)\n", e);
+    return HPDCT_MAPPING_AUTO;
+}
+
 std::mutex g_q_mutex;
 Mat64 g_q = [] {
     Mat64 m;
@@ -137,6 +149,15 @@ const char* hpdct_status_string(hpdct_status s) {
 }
 
 const char* hpdct_last_error_string(void) { return g_last_error.c_str(); }
+
+hpdct_status hpdct_set_mapping(hpdct_mapping mapping) {
+    if (mapping != HPDCT_MAPPING_AUTO && mapping != HPDCT_MAPPING_TILE && mapping != HPDCT_MAPPING_OCTET)
+        return HPDCT_ERROR_INVALID_VALUE;
+    g_mapping.store(static_cast<int>(mapping));
+    return HPDCT_SUCCESS;
+}
+
+hpdct_mapping hpdct_get_mapping(void) { return static_cast<hpdct_mapping>(hpdct::mapping_mode()); }
 
 void hpdct_default_quant_table(float* q64) {
     if (q64) memcpy(q64, kDefaultQ, sizeof(kDefaultQ));
@@ -348,3 +369,13 @@ void hpdct_f32_to_u8(const float* h_in, uint8_t* h_out, int64_t n) {
 }
 
 }  // extern "C"
+
+int hpdct::mapping_mode() {
+    int m = g_mapping.load(std::memory_order_relaxed);
+    if (m < 0) {
+        int expected = -1;
+        g_mapping.compare_exchange_strong(expected, mapping_from_env());
+        m = g_mapping.load();
+    }
+    return m;
+}

@@ -1,6 +1,6 @@
 // hpdct_fwd_f32.hip -- forward kernels with fp32 input (the reference's own
 // input type; compat path).  Kernels: hpdct_kernels_impl.hpp.
-#include "hpdct_kernels_impl.hpp"
+#include "hpdct_launch.hpp"
 
 namespace hpdct {
 #define HPDCT_FWD(TI, TO, QN, BT, WB)                                                                       \

@@ -1,6 +1,6 @@
 // hpdct_fwd_u8.hip -- forward kernels with uint8 input (one TU per input type
 // so the instantiations build in parallel).  Kernels: hpdct_kernels_impl.hpp.
-#include "hpdct_kernels_impl.hpp"
+#include "hpdct_launch.hpp"
 
 namespace hpdct {
 #define HPDCT_FWD(TI, TO, QN, BT, WB)                                                                       \

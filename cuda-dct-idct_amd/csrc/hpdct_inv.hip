@@ -1,5 +1,5 @@
 // hpdct_inv.hip -- inverse kernels.  Kernels: hpdct_kernels_impl.hpp.
-#include "hpdct_kernels_impl.hpp"
+#include "hpdct_launch.hpp"
 
 namespace hpdct {
 #define HPDCT_INV(TI, TO, DQ, BT)                                                                          \

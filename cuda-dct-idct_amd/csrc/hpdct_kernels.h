@@ -45,4 +45,7 @@ hipError_t launch_idct(const TIn* coef, TOut* out, float* dq_out, const TileGrid
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 
+// hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.
+int mapping_mode();
+
 }  // namespace hpdct

@@ -47,6 +47,9 @@ enum : unsigned {
     kVarNTLoad = 1u << 16,    // non-temporal loads of the 8-bit input planes
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
+    kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
+                                // all finite -> the zero terms of T are skipped (exact: a chain from +0
+                                // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
@@ -399,6 +402,20 @@ __device__ __forceinline__ float4* wave_slots() {
     }
 }
 
+// kVarFiniteSkip: true (wave-uniform) when every live lane's tile holds only
+// values with |v| < 2^125.  Then no operand is inf/NaN and no partial sum of
+// the first pass can overflow (|T row|_1 <= 8 * 0.7072 < 8), so the
+// products by the zero entries of T contribute exactly +0 to chains that
+// start from +0 and may be skipped; otherwise 0*inf / 0*NaN must produce NaN
+// as in the reference, and the full chain runs.
+__device__ __forceinline__ bool wave_tame(const float (&x)[8][8]) {
+    uint32_t m = 0;
+    unroll<8>([&](auto i) {
+        unroll<8>([&](auto j) { m = max(m, __float_as_uint(x[i][j]) & 0x7fffffffu); });
+    });
+    return __builtin_amdgcn_ballot_w64(m >= 0x7e000000u) == 0;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -442,6 +459,12 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
         };
         if constexpr ((kVar & kVarRowFirst) != 0) {
             fdct_tile_rowfirst(T, x, emit);
+        } else if constexpr ((kVar & kVarFiniteSkip) != 0 && kBuiltinT && !kSkipZero) {
+            if (wave_tame(x)) {
+                fdct_tile<(kVar & kVarRowMajor) != 0>(TSource<true, true>(t_dev), x, emit);
+            } else {
+                fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, emit);
+            }
         } else {
             fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, emit);
         }
@@ -479,6 +502,12 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(con
         };
         if constexpr ((kVar & kVarRowFirst) != 0) {
             idct_tile_rowfirst(T, d, emit);
+        } else if constexpr ((kVar & kVarFiniteSkip) != 0 && kBuiltinT && !kSkipZero) {
+            if (wave_tame(d)) {
+                idct_tile(TSource<true, true>(t_dev), d, emit);
+            } else {
+                idct_tile(T, d, emit);
+            }
         } else {
             idct_tile(T, d, emit);
         }
@@ -510,111 +539,6 @@ static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t
     } else {
         for (uint64_t i = i0; i < n; ++i) out[i] = static_cast<uint8_t>(hash_px(seed, first + i));
     }
-}
-
-// ---------------------------------------------------------------------------
-// Launch geometry.
-// ---------------------------------------------------------------------------
-// Resident waves per CU the persistent kernels are sized for (4 waves/SIMD at
-// <= 128 VGPRs); 256 CUs on MI355X.  The grid never exceeds the set count.
-constexpr uint32_t kPersistWavesPerCU = 16;
-
-inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t block = kBlockThreads) {
-    const uint32_t sets = (g.ntiles + 63u) / 64u;
-    const uint32_t waves_per_block = block / 64u;
-    uint32_t blocks = (sets + waves_per_block - 1) / waves_per_block;
-    if (persist) {
-        const uint32_t cap = cus * kPersistWavesPerCU / waves_per_block;
-        if (blocks > cap) blocks = cap;
-    }
-    return dim3(blocks);
-}
-
-inline uint32_t device_cus() {
-    static thread_local int cached_dev = -1;
-    static thread_local uint32_t cached_cus = 256;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 256;
-    if (dev != cached_dev) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            cached_cus = static_cast<uint32_t>(cus);
-        cached_dev = dev;
-    }
-    return cached_cus;
-}
-
-// Product variant choice (measured on MI355X, tools/kbench.hip):
-// fp32 planes are stored through the LDS re-staging with non-temporal
-// stores (1 KiB contiguous per store instruction), 8-bit planes with
-// non-temporal stores; the fast quotient where the caller proved it legal.
-// All product kernels use 512-thread workgroups (2u << 12: measured 1-3 %
-// faster than 256 on every kernel of the path, tools/kbench.hip).
-template <typename TIn, typename TOut>
-constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
-                              (std::is_same_v<TOut, int8_t> ? kVarI8Pack : 0u);
-
-template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
-hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev, const QParams& q,
-                   float shift, hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>), grid_for(g, false, 0, kBlock<kV>),
-                       dim3(kBlock<kV>), 0, s, img, out, shifted, g, t_dev, q, shift);
-    return hipGetLastError();
-}
-
-template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
-hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                            const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
-    constexpr unsigned kBase = kProdVar<TIn, TOut>;
-    if constexpr (std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback) {
-        if (fastdiv)
-            return fdct_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
-                                                                                          q, shift, s);
-    }
-    if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
-        if (row_first)
-            return fdct_go<kBase | kVarRowFirst, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
-                                                                                           t_dev, q, shift, s);
-    }
-    (void)fastdiv;
-    (void)row_first;
-    return fdct_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
-}
-
-template <unsigned kV, typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-hipError_t idct_go(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev, const Mat64& q,
-                   float shift, hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), grid_for(g, false, 0, kBlock<kV>),
-                       dim3(kBlock<kV>), 0, s, coef, out, dq_out, g, t_dev, q, shift);
-    return hipGetLastError();
-}
-
-template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
-hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
-                            const Mat64& q, float shift, bool row_first, hipStream_t s) {
-    constexpr unsigned kV = kProdVar<TIn, TOut>;
-    if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
-        if constexpr (kDequant) {
-            if (dq_out && row_first)
-                return idct_go<kV | kVarRowFirst | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g,
-                                                                                                 t_dev, q, shift, s);
-            if (dq_out)
-                return idct_go<kV | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q,
-                                                                                   shift, s);
-        }
-        if (row_first)
-            return idct_go<kV | kVarRowFirst, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
-                                                                              s);
-    }
-    (void)row_first;
-    return idct_go<kV, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
-}
-
-inline hipError_t launch_fill_hash_impl(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {
-    const uint64_t lanes = (n + 15) / 16;
-    const dim3 grid(static_cast<uint32_t>((lanes + kBlockThreads - 1) / kBlockThreads));
-    hipLaunchKernelGGL(fill_hash_kernel, grid, dim3(kBlockThreads), 0, s, out, n, seed, first);
-    return hipGetLastError();
 }
 
 }  // namespace hpdct

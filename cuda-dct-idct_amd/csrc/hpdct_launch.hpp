@@ -1,0 +1,173 @@
+// hpdct_launch.hpp -- launch geometry and the product's kernel choice for
+// every (input, output, flags) combination of the path.  Included by the
+// explicit-instantiation units (hpdct_fwd_*.hip, hpdct_inv.hip) and tools.
+#pragma once
+
+#include "hpdct_kernels_impl.hpp"
+#include "hpdct_octet.hpp"
+
+namespace hpdct {
+
+// ---------------------------------------------------------------------------
+// Launch geometry.
+// ---------------------------------------------------------------------------
+// Resident waves per CU the persistent kernels are sized for (4 waves/SIMD at
+// <= 128 VGPRs); 256 CUs on MI355X.  The grid never exceeds the set count.
+constexpr uint32_t kPersistWavesPerCU = 16;
+
+inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t block = kBlockThreads) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u;
+    const uint32_t waves_per_block = block / 64u;
+    uint32_t blocks = (sets + waves_per_block - 1) / waves_per_block;
+    if (persist) {
+        const uint32_t cap = cus * kPersistWavesPerCU / waves_per_block;
+        if (blocks > cap) blocks = cap;
+    }
+    return dim3(blocks);
+}
+
+inline uint32_t device_cus() {
+    static thread_local int cached_dev = -1;
+    static thread_local uint32_t cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev != cached_dev) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            cached_cus = static_cast<uint32_t>(cus);
+        cached_dev = dev;
+    }
+    return cached_cus;
+}
+
+// Product variant choice (measured on MI355X, tools/kbench.hip).
+//
+// Tile-per-lane kernels (hpdct_kernels_impl.hpp), for frames of >= 8 tile
+// sets (64 tiles each) per CU: fp32 planes are stored through the LDS
+// re-staging with non-temporal stores (1 KiB contiguous per store
+// instruction), 8-bit planes with non-temporal stores; the int8 output with
+// the SDWA byte-pack conversion; the fast quotient where the caller proved it
+// legal.  512-thread workgroups (1-3 % faster than 256 on every kernel).
+template <typename TIn, typename TOut>
+constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
+                              (std::is_same_v<TOut, int8_t> ? kVarI8Pack : 0u);
+// Octet kernels (hpdct_octet.hpp, 8 lanes per tile) for smaller frames,
+// where the tile-per-lane grid is too short to fill 256 CUs (1024^2: 6.2 ->
+// 3.7 us), and for the fp32 -> fp32 inverse at every size (8192^2: 98.8 ->
+// 92.8 us).  256-thread workgroups; fp32 rows re-staged for 256-B runs.
+template <typename TOut>
+constexpr unsigned kOctVar = kVarNT | (std::is_same_v<TOut, float> ? kOctRestage : 0u);
+constexpr uint32_t kOctetSetsPerCU = 8;
+
+// prefer: the octet mapping also wins at large frames for this kernel
+inline bool use_octet(const TileGrid& g, bool prefer = false) {
+    const int m = mapping_mode();
+    if (m == 1) return false;  // HPDCT_MAPPING_TILE
+    if (m == 2) return true;   // HPDCT_MAPPING_OCTET
+    return prefer || (g.ntiles + 63u) / 64u < kOctetSetsPerCU * device_cus();
+}
+
+template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev, const QParams& q,
+                   float shift, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>), grid_for(g, false, 0, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, img, out, shifted, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
+template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t fdct_octet_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
+                         const QParams& q, float shift, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_octet_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>), octet_grid(g, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, img, out, shifted, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
+template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
+                            const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
+    constexpr unsigned kBase = kProdVar<TIn, TOut>;
+    constexpr unsigned kOct = kOctVar<TOut>;
+    constexpr bool kFastDivOk = std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback;
+    if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
+        if (row_first)  // cublasDCTv2 pass order: tile-per-lane only
+            return fdct_go<kBase | kVarRowFirst, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
+                                                                                           t_dev, q, shift, s);
+    }
+    (void)row_first;
+    if (use_octet(g)) {
+        if constexpr (kFastDivOk) {
+            if (fastdiv)
+                return fdct_octet_go<kOct | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+                    img, out, shifted, g, t_dev, q, shift, s);
+        }
+        return fdct_octet_go<kOct, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift,
+                                                                             s);
+    }
+    if constexpr (kFastDivOk) {
+        if (fastdiv)
+            return fdct_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
+                                                                                          q, shift, s);
+    }
+    (void)fastdiv;
+    return fdct_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+}
+
+template <unsigned kV, typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
+hipError_t idct_go(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev, const Mat64& q,
+                   float shift, hipStream_t s) {
+    hipLaunchKernelGGL((idct_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), grid_for(g, false, 0, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, coef, out, dq_out, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
+template <unsigned kV, typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
+hipError_t idct_octet_go(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
+                         const Mat64& q, float shift, hipStream_t s) {
+    hipLaunchKernelGGL((idct_octet_kernel<TIn, TOut, kDequant, kBuiltinT, kV>), octet_grid(g, kBlock<kV>),
+                       dim3(kBlock<kV>), 0, s, coef, out, dq_out, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
+template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
+hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
+                            const Mat64& q, float shift, bool row_first, hipStream_t s) {
+    constexpr unsigned kV = kProdVar<TIn, TOut>;
+    constexpr unsigned kOct = kOctVar<TOut>;
+    constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
+    if constexpr (kF32) {
+        if (row_first) {  // cublasDCTv2 pass order: tile-per-lane only
+            if constexpr (kDequant) {
+                if (dq_out)
+                    return idct_go<kV | kVarRowFirst | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(
+                        coef, out, dq_out, g, t_dev, q, shift, s);
+            }
+            return idct_go<kV | kVarRowFirst, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
+                                                                              s);
+        }
+    }
+    (void)row_first;
+    if (use_octet(g, kF32)) {
+        if constexpr (kF32 && kDequant) {
+            if (dq_out)
+                return idct_octet_go<kOct | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g,
+                                                                                          t_dev, q, shift, s);
+        }
+        return idct_octet_go<kOct, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
+    }
+    if constexpr (kF32 && kDequant) {  // HPDCT_MAPPING_TILE
+        if (dq_out)
+            return idct_go<kV | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
+                                                                               s);
+    }
+    return idct_go<kV, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
+}
+
+inline hipError_t launch_fill_hash_impl(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {
+    const uint64_t lanes = (n + 15) / 16;
+    const dim3 grid(static_cast<uint32_t>((lanes + kBlockThreads - 1) / kBlockThreads));
+    hipLaunchKernelGGL(fill_hash_kernel, grid, dim3(kBlockThreads), 0, s, out, n, seed, first);
+    return hipGetLastError();
+}
+
+}  // namespace hpdct

@@ -48,8 +48,9 @@ C_SYMBOLS = [
     "hpdct_forward", "hpdct_inverse",
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
-    "hpdct_baseline_forward", "hpdct_stream_forward",
+    "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
 ]
+MAPPINGS = {"auto": 0, "tile": 1, "octet": 2}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
 COMPAT_SYMBOLS = {
     "dct_all_blocks_cuda": "_Z19dct_all_blocks_cudaPfiiPKfS_",
@@ -119,6 +120,10 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_u8_to_f32.restype = None
     lib.hpdct_f32_to_u8.argtypes = [vp, vp, i64]
     lib.hpdct_f32_to_u8.restype = None
+    lib.hpdct_set_mapping.argtypes = [ctypes.c_int]
+    lib.hpdct_set_mapping.restype = ctypes.c_int
+    lib.hpdct_get_mapping.argtypes = []
+    lib.hpdct_get_mapping.restype = ctypes.c_int
     lib.hpdct_stream_forward.argtypes = [vp, vp, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp]
     lib.hpdct_stream_forward.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
@@ -140,6 +145,20 @@ def _check(status: int) -> None:
 
 def version() -> str:
     return load_library().hpdct_version().decode()
+
+
+def set_mapping(name: str) -> None:
+    """Kernel work mapping, process-wide: "auto" (per frame size), "tile"
+    (one lane per 8x8 tile) or "octet" (eight lanes per tile).  Results are
+    bit-identical; for A/B timing and tests (include/hpdct.h)."""
+    if name not in MAPPINGS:
+        raise ValueError(f"mapping must be one of {sorted(MAPPINGS)}")
+    _check(load_library().hpdct_set_mapping(MAPPINGS[name]))
+
+
+def get_mapping() -> str:
+    m = load_library().hpdct_get_mapping()
+    return {v: k for k, v in MAPPINGS.items()}[m]
 
 
 # ---------------------------------------------------------------------------

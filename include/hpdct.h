@@ -140,6 +140,24 @@ hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h
  * oracle_fill_hash_u8 restates it). */
 hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_t first_index, void* stream);
 
+/* Work mapping of the kernels (new; the reference has one fixed decomposition
+ * per program).  Output is bit-identical in every mapping; only speed differs.
+ *   AUTO   per frame: eight lanes per 8x8 tile ("octet") for frames below
+ *          8 x 64-tile sets per CU and for the fp32 -> fp32 inverse, one lane
+ *          per tile otherwise (DESIGN.md "Kernels").
+ *   TILE   one lane per tile always.     OCTET  eight lanes per tile always.
+ * The cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST) always runs one lane per
+ * tile.  Process-wide; the initial value comes from the environment variable
+ * HPDCT_MAPPING ("auto", "tile", "octet"), else AUTO.  For A/B measurement
+ * and tests; set it while no call is in flight. */
+typedef enum hpdct_mapping {
+    HPDCT_MAPPING_AUTO = 0,
+    HPDCT_MAPPING_TILE = 1,
+    HPDCT_MAPPING_OCTET = 2
+} hpdct_mapping;
+hpdct_status hpdct_set_mapping(hpdct_mapping mapping);
+hpdct_mapping hpdct_get_mapping(void);
+
 /* Host-side helpers (no device work). */
 void hpdct_fill_rand_u8(uint8_t* h_out, int64_t n, uint32_t seed); /* srand(seed); rand()%256 (glibc TYPE_3) */
 void hpdct_u8_to_f32(const uint8_t* h_in, float* h_out, int64_t n); /* convertToFloat, utils.cu:10-15 */

@@ -111,6 +111,33 @@ def test_quant_table_state(hp):
     assert np.array_equal(hp.get_quant_table(), hp.default_quant_table())
 
 
+def test_mapping_state(hp):
+    assert hp.get_mapping() == "auto"
+    try:
+        for m in ("tile", "octet", "auto"):
+            hp.set_mapping(m)
+            assert hp.get_mapping() == m
+        assert hp.load_library().hpdct_set_mapping(7) == 1  # HPDCT_ERROR_INVALID_VALUE
+        assert hp.get_mapping() == "auto"
+        with pytest.raises(ValueError):
+            hp.set_mapping("wave")
+    finally:
+        hp.set_mapping("auto")
+
+
+def test_mapping_from_environment(tmp_path):
+    """HPDCT_MAPPING seeds the process-wide mapping (the GPU tests' child
+    processes rely on it); an unknown value falls back to auto."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import hpdct; print(hpdct.get_mapping())"
+            % os.path.join(ROOT, "cuda-dct-idct_amd"))
+    for env_val, want in (("octet", "octet"), ("tile", "tile"), ("bogus", "auto")):
+        env = dict(os.environ, HPDCT_MAPPING=env_val)
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        assert out.stdout.strip() == want
+
+
 @pytest.mark.parametrize("h,w", [(0, 8), (8, 0), (12, 8), (8, 20), (-8, 8), (7, 7)])
 def test_bad_shapes_rejected_before_device_work(hp, h, w):
     L = hp.load_library()

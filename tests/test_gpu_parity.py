@@ -35,6 +35,17 @@ def mismatches(a, b):
     return int((np.ascontiguousarray(a, np.float32).view(np.uint32) != np.ascontiguousarray(b, np.float32).view(np.uint32)).sum())
 
 
+@pytest.fixture(autouse=True, params=["tile", "octet"])
+def mapping(request, hp, monkeypatch):
+    """Every parity case runs under both work mappings (one lane per tile,
+    eight lanes per tile); child processes inherit HPDCT_MAPPING.  AUTO picks
+    one of the two per frame size, so both forced runs cover it."""
+    monkeypatch.setenv("HPDCT_MAPPING", request.param)
+    hp.set_mapping(request.param)
+    yield request.param
+    hp.set_mapping("auto")
+
+
 @pytest.fixture(scope="module")
 def golden():
     with open(os.path.join(GOLD, "golden.json")) as fh:

@@ -17,7 +17,7 @@
 #include <string>
 #include <vector>
 
-#include "hpdct_kernels_impl.hpp"
+#include "hpdct_launch.hpp"
 
 using namespace hpdct;
 
@@ -169,7 +169,20 @@ void launch_inv_any(const uint8_t* in, float* out, const TileGrid& g, const QPar
                     hipStream_t s) {
     hipLaunchKernelGGL((idct_kernel<TI, TO, true, true, kVar>), grid_for(g, false, cus, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s,
-                       reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), g, nullptr, qp.q, 128.0f);
+                       reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr, g, nullptr, qp.q, 128.0f);
+}
+
+template <typename TI, typename TO, unsigned kVar>
+void launch_fwd_oct(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_octet_kernel<TI, TO, true, true, false, kVar>), octet_grid(g, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr,
+                       g, nullptr, qp, 128.0f);
+}
+template <typename TI, typename TO, unsigned kVar>
+void launch_inv_oct(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL((idct_octet_kernel<TI, TO, true, true, kVar>), octet_grid(g, kBlock<kVar>), dim3(kBlock<kVar>),
+                       0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr, g, nullptr, qp.q,
+                       128.0f);
 }
 
 void launch_copy_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
@@ -219,16 +232,29 @@ int main(int argc, char** argv) {
     constexpr unsigned B = L | N | F, R = kVarRowMajor, S = kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
     constexpr unsigned LL = kVarLdsLoad;
     constexpr unsigned NL = kVarNTLoad, IP = kVarI8Pack;
+    constexpr unsigned OR = kOctRestage;
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
         {"product (b512+lds+nt+fast)", launch_var<B | W512>},
-        {"product + nt loads", launch_var<B | W512 | NL>},
+        {"octet u8 b256", launch_fwd_oct<uint8_t, float, F | N>},
+        {"octet u8 b256 restage", launch_fwd_oct<uint8_t, float, F | N | OR>},
+        {"octet u8 b512 restage", launch_fwd_oct<uint8_t, float, F | N | OR | W512>},
     };
     std::vector<Variant> other = {
-        {"fwd u8->i8 +i8pack", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
-        {"fwd u8->i8 +i8pack+xor", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP | X>},
-        {"fwd u8->i8 +i8pack no-nt", launch_fwd_any<uint8_t, int8_t, F | W512 | IP>},
-        {"fwd u8->i8 +i8pack b256", launch_fwd_any<uint8_t, int8_t, F | N | IP>},
+        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32 octet b256", launch_fwd_oct<float, float, N>, true},
+        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32 octet b256 restage", launch_fwd_oct<float, float, N | OR>, true},
+        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32 octet b512 restage", launch_fwd_oct<float, float, N | OR | W512>, true},
+        {"inv f32 product", launch_inv_any<float, float, L | N | W512>, true},
+        {"inv f32 octet b256", launch_inv_oct<float, float, N>, true},
+        {"inv f32 product", launch_inv_any<float, float, L | N | W512>, true},
+        {"inv f32 octet b256 restage", launch_inv_oct<float, float, N | OR>, true},
+        {"inv i8->u8 product", launch_inv_any<int8_t, uint8_t, N | W512>},
+        {"inv i8->u8 octet b256", launch_inv_oct<int8_t, uint8_t, N>},
+        {"fwd u8->i8 product", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 octet b256", launch_fwd_oct<uint8_t, int8_t, F | N>},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
@@ -270,14 +296,16 @@ int main(int argc, char** argv) {
         for (size_t v = 0; v < vars.size(); ++v) {
             auto src = [&](int i) { return vars[v].f32_input ? inf[i % nsets] : in[i % nsets]; };
             for (int w = 0; w < 5; ++w) vars[v].launch(src(w), out[w % nsets], g, qp, cus, 0);
-            for (int i = 0; i < iters; ++i) {
+            // back-to-back region (no per-launch sync: small frames would time the
+            // launch latency), average per launch; repeated in blocks of nsets
+            for (int i = 0; i < iters; i += nsets) {
                 CK(hipEventRecord(a, 0));
-                vars[v].launch(src(i), out[i % nsets], g, qp, cus, 0);
+                for (int k = 0; k < 8 * nsets; ++k) vars[v].launch(src(k), out[k % nsets], g, qp, cus, 0);
                 CK(hipEventRecord(b, 0));
                 CK(hipEventSynchronize(b));
                 float ms = 0;
                 CK(hipEventElapsedTime(&ms, a, b));
-                us[v].push_back(ms * 1e3f);
+                for (int k = 0; k < nsets; ++k) us[v].push_back(ms * 1e3f / (8 * nsets));
             }
         }
     }
