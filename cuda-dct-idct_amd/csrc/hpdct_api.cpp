@@ -53,7 +53,8 @@ int mapping_from_env() {
     if (!e || !*e || strcmp(e, "auto") == 0) return HPDCT_MAPPING_AUTO;
     if (strcmp(e, "tile") == 0) return HPDCT_MAPPING_TILE;
     if (strcmp(e, "octet") == 0) return HPDCT_MAPPING_OCTET;
-    fprintf(stderr, "hpdct: ignoring HPDCT_MAPPING=%s (expected auto, tile or octet)\n", e);
+    if (strcmp(e, "duo") == 0) return HPDCT_MAPPING_DUO;
+    fprintf(stderr, "hpdct: ignoring HPDCT_MAPPING=%s (expected auto, tile, octet or duo)\n", e);
     return HPDCT_MAPPING_AUTO;
 }
 
@@ -151,7 +152,8 @@ const char* hpdct_status_string(hpdct_status s) {
 const char* hpdct_last_error_string(void) { return g_last_error.c_str(); }
 
 hpdct_status hpdct_set_mapping(hpdct_mapping mapping) {
-    if (mapping != HPDCT_MAPPING_AUTO && mapping != HPDCT_MAPPING_TILE && mapping != HPDCT_MAPPING_OCTET)
+    if (mapping != HPDCT_MAPPING_AUTO && mapping != HPDCT_MAPPING_TILE && mapping != HPDCT_MAPPING_OCTET &&
+        mapping != HPDCT_MAPPING_DUO)
         return HPDCT_ERROR_INVALID_VALUE;
     g_mapping.store(static_cast<int>(mapping));
     return HPDCT_SUCCESS;

@@ -3,8 +3,10 @@
 // explicit-instantiation units (hpdct_fwd_*.hip, hpdct_inv.hip) and tools.
 #pragma once
 
+#include "hpdct.h"
 #include "hpdct_kernels_impl.hpp"
 #include "hpdct_octet.hpp"
+#include "hpdct_duo.hpp"
 
 namespace hpdct {
 
@@ -53,18 +55,25 @@ constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float>
                               (std::is_same_v<TOut, int8_t> ? kVarI8Pack : 0u);
 // Octet kernels (hpdct_octet.hpp, 8 lanes per tile) for smaller frames,
 // where the tile-per-lane grid is too short to fill 256 CUs (1024^2: 6.2 ->
-// 3.7 us), and for the fp32 -> fp32 inverse at every size (8192^2: 98.8 ->
-// 92.8 us).  256-thread workgroups; fp32 rows re-staged for 256-B runs.
+// 3.7 us).  256-thread workgroups; fp32 rows re-staged for 256-B runs.
 template <typename TOut>
 constexpr unsigned kOctVar = kVarNT | (std::is_same_v<TOut, float> ? kOctRestage : 0u);
 constexpr uint32_t kOctetSetsPerCU = 8;
+// Duo kernels (hpdct_duo.hpp, 2 lanes per tile, 1 KiB row loads and stores)
+// for fp32 -> fp32 at the other sizes (8192^2: forward 102.4 -> 89.6 us,
+// inverse 93.3 -> 88.0 us, compat forward with write-back 159 -> 136 us).
+constexpr unsigned kDuoVar = kVarNT;
 
-// prefer: the octet mapping also wins at large frames for this kernel
-inline bool use_octet(const TileGrid& g, bool prefer = false) {
+enum class Mapping { kTile, kOctet, kDuo };
+
+// f32: an fp32 -> fp32 kernel in the reference's pass order (duo-capable)
+inline Mapping pick_mapping(const TileGrid& g, bool f32) {
     const int m = mapping_mode();
-    if (m == 1) return false;  // HPDCT_MAPPING_TILE
-    if (m == 2) return true;   // HPDCT_MAPPING_OCTET
-    return prefer || (g.ntiles + 63u) / 64u < kOctetSetsPerCU * device_cus();
+    if (m == HPDCT_MAPPING_TILE) return Mapping::kTile;
+    if (m == HPDCT_MAPPING_OCTET) return Mapping::kOctet;
+    if (m == HPDCT_MAPPING_DUO && f32) return Mapping::kDuo;
+    if ((g.ntiles + 63u) / 64u < kOctetSetsPerCU * device_cus()) return Mapping::kOctet;
+    return f32 ? Mapping::kDuo : Mapping::kTile;
 }
 
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
@@ -83,6 +92,22 @@ hipError_t fdct_octet_go(const TIn* img, TOut* out, float* shifted, const TileGr
     return hipGetLastError();
 }
 
+template <unsigned kV, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t fdct_duo_go(const float* img, float* out, float* shifted, const TileGrid& g, const float* t_dev,
+                       const QParams& q, float shift, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_duo_kernel<kQuant, kBuiltinT, kWriteback, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>),
+                       0, s, img, out, shifted, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
+template <unsigned kV, bool kDequant, bool kBuiltinT>
+hipError_t idct_duo_go(const float* coef, float* out, float* dq_out, const TileGrid& g, const float* t_dev,
+                       const Mat64& q, float shift, hipStream_t s) {
+    hipLaunchKernelGGL((idct_duo_kernel<kDequant, kBuiltinT, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>), 0, s,
+                       coef, out, dq_out, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                             const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
@@ -95,7 +120,13 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
                                                                                            t_dev, q, shift, s);
     }
     (void)row_first;
-    if (use_octet(g)) {
+    constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
+    const Mapping map = pick_mapping(g, kF32);
+    if constexpr (kF32) {
+        if (map == Mapping::kDuo)
+            return fdct_duo_go<kDuoVar, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+    }
+    if (map == Mapping::kOctet) {
         if constexpr (kFastDivOk) {
             if (fastdiv)
                 return fdct_octet_go<kOct | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
@@ -147,7 +178,18 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
         }
     }
     (void)row_first;
-    if (use_octet(g, kF32)) {
+    const Mapping map = pick_mapping(g, kF32);
+    if constexpr (kF32) {
+        if (map == Mapping::kDuo) {
+            if constexpr (kDequant) {
+                if (dq_out)
+                    return idct_duo_go<kDuoVar | kVarWbDequant, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q,
+                                                                                   shift, s);
+            }
+            return idct_duo_go<kDuoVar, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
+        }
+    }
+    if (map == Mapping::kOctet) {
         if constexpr (kF32 && kDequant) {
             if (dq_out)
                 return idct_octet_go<kOct | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g,
@@ -155,7 +197,7 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
         }
         return idct_octet_go<kOct, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
     }
-    if constexpr (kF32 && kDequant) {  // HPDCT_MAPPING_TILE
+    if constexpr (kF32 && kDequant) {
         if (dq_out)
             return idct_go<kV | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
                                                                                s);

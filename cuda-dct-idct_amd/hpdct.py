@@ -50,7 +50,7 @@ C_SYMBOLS = [
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
 ]
-MAPPINGS = {"auto": 0, "tile": 1, "octet": 2}
+MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
 COMPAT_SYMBOLS = {
     "dct_all_blocks_cuda": "_Z19dct_all_blocks_cudaPfiiPKfS_",
@@ -149,8 +149,9 @@ def version() -> str:
 
 def set_mapping(name: str) -> None:
     """Kernel work mapping, process-wide: "auto" (per frame size), "tile"
-    (one lane per 8x8 tile) or "octet" (eight lanes per tile).  Results are
-    bit-identical; for A/B timing and tests (include/hpdct.h)."""
+    (one lane per 8x8 tile), "octet" (eight lanes per tile) or "duo" (two
+    lanes per tile, fp32 -> fp32 kernels).  Results are bit-identical; for
+    A/B timing and tests (include/hpdct.h)."""
     if name not in MAPPINGS:
         raise ValueError(f"mapping must be one of {sorted(MAPPINGS)}")
     _check(load_library().hpdct_set_mapping(MAPPINGS[name]))

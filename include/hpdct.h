@@ -143,17 +143,19 @@ hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_
 /* Work mapping of the kernels (new; the reference has one fixed decomposition
  * per program).  Output is bit-identical in every mapping; only speed differs.
  *   AUTO   per frame: eight lanes per 8x8 tile ("octet") for frames below
- *          8 x 64-tile sets per CU and for the fp32 -> fp32 inverse, one lane
- *          per tile otherwise (DESIGN.md "Kernels").
+ *          8 x 64-tile sets per CU; above that two lanes per tile ("duo") for
+ *          fp32 -> fp32, one lane per tile for the rest (DESIGN.md "Kernels").
  *   TILE   one lane per tile always.     OCTET  eight lanes per tile always.
+ *   DUO    two lanes per tile for every fp32 -> fp32 kernel, AUTO otherwise.
  * The cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST) always runs one lane per
  * tile.  Process-wide; the initial value comes from the environment variable
- * HPDCT_MAPPING ("auto", "tile", "octet"), else AUTO.  For A/B measurement
- * and tests; set it while no call is in flight. */
+ * HPDCT_MAPPING ("auto", "tile", "octet", "duo"), else AUTO.  For A/B
+ * measurement and tests; set it while no call is in flight. */
 typedef enum hpdct_mapping {
     HPDCT_MAPPING_AUTO = 0,
     HPDCT_MAPPING_TILE = 1,
-    HPDCT_MAPPING_OCTET = 2
+    HPDCT_MAPPING_OCTET = 2,
+    HPDCT_MAPPING_DUO = 3
 } hpdct_mapping;
 hpdct_status hpdct_set_mapping(hpdct_mapping mapping);
 hpdct_mapping hpdct_get_mapping(void);

@@ -114,7 +114,7 @@ def test_quant_table_state(hp):
 def test_mapping_state(hp):
     assert hp.get_mapping() == "auto"
     try:
-        for m in ("tile", "octet", "auto"):
+        for m in ("tile", "octet", "duo", "auto"):
             hp.set_mapping(m)
             assert hp.get_mapping() == m
         assert hp.load_library().hpdct_set_mapping(7) == 1  # HPDCT_ERROR_INVALID_VALUE
@@ -132,7 +132,7 @@ def test_mapping_from_environment(tmp_path):
     import sys
     code = ("import sys; sys.path.insert(0, %r); import hpdct; print(hpdct.get_mapping())"
             % os.path.join(ROOT, "cuda-dct-idct_amd"))
-    for env_val, want in (("octet", "octet"), ("tile", "tile"), ("bogus", "auto")):
+    for env_val, want in (("octet", "octet"), ("tile", "tile"), ("duo", "duo"), ("bogus", "auto")):
         env = dict(os.environ, HPDCT_MAPPING=env_val)
         out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
         assert out.stdout.strip() == want

@@ -35,11 +35,11 @@ def mismatches(a, b):
     return int((np.ascontiguousarray(a, np.float32).view(np.uint32) != np.ascontiguousarray(b, np.float32).view(np.uint32)).sum())
 
 
-@pytest.fixture(autouse=True, params=["tile", "octet"])
+@pytest.fixture(autouse=True, params=["tile", "octet", "duo"])
 def mapping(request, hp, monkeypatch):
-    """Every parity case runs under both work mappings (one lane per tile,
-    eight lanes per tile); child processes inherit HPDCT_MAPPING.  AUTO picks
-    one of the two per frame size, so both forced runs cover it."""
+    """Every parity case runs under each forced work mapping (one, eight or,
+    for fp32 -> fp32, two lanes per tile); child processes inherit
+    HPDCT_MAPPING.  AUTO picks among these per frame size."""
     monkeypatch.setenv("HPDCT_MAPPING", request.param)
     hp.set_mapping(request.param)
     yield request.param

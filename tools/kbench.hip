@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "hpdct_launch.hpp"
+#include "hpdct_duo.hpp"
 
 using namespace hpdct;
 
@@ -185,6 +186,32 @@ void launch_inv_oct(const uint8_t* in, float* out, const TileGrid& g, const QPar
                        128.0f);
 }
 
+// compat-path shape: runtime T (device buffer), X-128 written back (to a scratch plane here)
+float* g_T = nullptr;
+float* g_wb = nullptr;
+template <unsigned kVar>
+void launch_fwd_compat_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                            hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<float, float, true, false, true, kVar>), grid_for(g, false, 0, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
+}
+template <unsigned kVar>
+void launch_fwd_compat_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((fdct_duo_kernel<true, false, true, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
+}
+template <unsigned kVar>
+void launch_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_duo_kernel<true, true, false, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp, 128.0f);
+}
+template <unsigned kVar>
+void launch_inv_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL((idct_duo_kernel<true, true, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp.q, 128.0f);
+}
+
 void launch_copy_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL(copy_tilepattern, dim3((g.ntiles + 255) / 256), dim3(256), 0, s, in, out, g);
 }
@@ -212,6 +239,13 @@ int main(int argc, char** argv) {
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
 
+    {
+        float th[64];
+        for (int i = 0; i < 64; ++i) th[i] = kBuiltinT.v[i];
+        CK(hipMalloc(&g_T, sizeof(th)));
+        CK(hipMemcpy(g_T, th, sizeof(th), hipMemcpyHostToDevice));
+        CK(hipMalloc(&g_wb, px * 4));
+    }
     std::vector<uint8_t*> in(nsets), inf(nsets);
     std::vector<float*> out(nsets);
     std::vector<uint8_t> h(px);
@@ -242,19 +276,17 @@ int main(int argc, char** argv) {
     };
     std::vector<Variant> other = {
         {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 octet b256", launch_fwd_oct<float, float, N>, true},
+        {"fwd f32 duo b256", launch_fwd_duo<N>, true},
         {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 octet b256 restage", launch_fwd_oct<float, float, N | OR>, true},
+        {"fwd f32 duo b512", launch_fwd_duo<N | W512>, true},
         {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 octet b512 restage", launch_fwd_oct<float, float, N | OR | W512>, true},
-        {"inv f32 product", launch_inv_any<float, float, L | N | W512>, true},
-        {"inv f32 octet b256", launch_inv_oct<float, float, N>, true},
-        {"inv f32 product", launch_inv_any<float, float, L | N | W512>, true},
-        {"inv f32 octet b256 restage", launch_inv_oct<float, float, N | OR>, true},
-        {"inv i8->u8 product", launch_inv_any<int8_t, uint8_t, N | W512>},
-        {"inv i8->u8 octet b256", launch_inv_oct<int8_t, uint8_t, N>},
-        {"fwd u8->i8 product", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
-        {"fwd u8->i8 octet b256", launch_fwd_oct<uint8_t, int8_t, F | N>},
+        {"fwd f32 duo b256 plain-st", launch_fwd_duo<0>, true},
+        {"inv f32 octet (product)", launch_inv_oct<float, float, N | OR>, true},
+        {"inv f32 duo b256", launch_inv_duo<N>, true},
+        {"inv f32 octet (product)", launch_inv_oct<float, float, N | OR>, true},
+        {"inv f32 duo b512", launch_inv_duo<N | W512>, true},
+        {"compat fwd tile (product)", launch_fwd_compat_tile<L | N | W512>, true},
+        {"compat fwd duo b256", launch_fwd_compat_duo<N>, true},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
