@@ -47,6 +47,8 @@ enum : unsigned {
     kVarNTLoad = 1u << 16,    // non-temporal loads of the 8-bit input planes
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
+    kVarPacked = 1u << 19,      // uint8 input, built-in T, quantised: packed-fp32 transform and quotient
+                                // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, fdct_tile_pk)
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
                                 // all finite -> the zero terms of T are skipped (exact: a chain from +0
                                 // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
@@ -117,6 +119,25 @@ __device__ __forceinline__ uint32_t pack_q_i8x4(float a, float b, float c, float
     asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
                  : "+v"(w) : "v"(biased(d)));
     return w;
+}
+
+// v_cvt_i32_f32 (truncating) of an already-biased value straight into byte
+// kByte of w, the other bytes preserved (SDWA dst_sel).
+template <int kByte>
+__device__ __forceinline__ void cvt_into_byte(uint32_t& w, float biased) {
+    static_assert(kByte >= 0 && kByte < 4, "byte");
+    if constexpr (kByte == 0)
+        asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                     : "+v"(w) : "v"(biased));
+    else if constexpr (kByte == 1)
+        asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                     : "+v"(w) : "v"(biased));
+    else if constexpr (kByte == 2)
+        asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                     : "+v"(w) : "v"(biased));
+    else
+        asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                     : "+v"(w) : "v"(biased));
 }
 
 // divide_matrices (utils_kernels.cu:42): round(C / Q)
@@ -435,6 +456,52 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
 
     walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
                                                       uint64_t seg) {
+        if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && kBuiltinT && kQuant &&
+                      !kWriteback && (kVar & kVarRowFirst) == 0) {
+            float xs[8][8];
+            raw.to_float(xs, 0.0f);
+            f32x2 x2[8][4];
+            unroll<8>([&](auto i) {
+                unroll<4>([&](auto cp) { x2[i][cp] = f32x2{xs[i][2 * cp], xs[i][2 * cp + 1]} - f32x2{shift, shift}; });
+            });
+            fdct_tile_pk(x2, [&](auto v, f32x2(&c2)[4]) {
+                // quotient per pair: the verified 3-op form (packed) or IEEE division
+                f32x2 d2[4];
+                unroll<4>([&](auto k) {
+                    constexpr int u0 = kPairU[k][0], u1 = kPairU[k][1];
+                    const f32x2 q2 = {qp.q.v[v * 8 + u0], qp.q.v[v * 8 + u1]};
+                    if constexpr ((kVar & kVarFastDiv) != 0) {
+                        const f32x2 r2 = {qp.r.v[v * 8 + u0], qp.r.v[v * 8 + u1]};
+                        const f32x2 q0 = c2[k] * r2;
+                        const f32x2 e = fma2(-q0, q2, c2[k]);
+                        d2[k] = fma2(e, r2, q0);
+                    } else {
+                        d2[k] = f32x2{c2[k].x / q2.x, c2[k].y / q2.y};
+                    }
+                    // round half away: trunc(d + copysign(0.49999997, d)) (verify_round3.c)
+                    d2[k] = d2[k] + f32x2{__builtin_copysignf(0.49999997f, d2[k].x),
+                                          __builtin_copysignf(0.49999997f, d2[k].y)};
+                });
+                if constexpr (std::is_same_v<TOut, int8_t>) {
+                    uint32_t w[2] = {0u, 0u};
+                    unroll<4>([&](auto k) {
+                        constexpr int u0 = kPairU[k][0], u1 = kPairU[k][1];
+                        cvt_into_byte<u0 % 4>(w[u0 / 4], d2[k].x);
+                        cvt_into_byte<u1 % 4>(w[u1 / 4], d2[k].y);
+                    });
+                    st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width),
+                                             make_uint2(w[0], w[1]));
+                } else {
+                    float c[8];
+                    unroll<4>([&](auto k) {
+                        c[kPairU[k][0]] = __builtin_truncf(d2[k].x);
+                        c[kPairU[k][1]] = __builtin_truncf(d2[k].y);
+                    });
+                    sink(v, p, ok, seg, c);
+                }
+            });
+            return;
+        }
         float x[8][8];
         if constexpr ((kVar & kVarXorCvt) != 0 && std::is_same_v<TIn, uint8_t>) {
             raw.to_float_minus128(x);  // launcher guarantees shift == 128

@@ -212,6 +212,14 @@ void launch_inv_duo(const uint8_t* in, float* out, const TileGrid& g, const QPar
                        reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp.q, 128.0f);
 }
 
+template <typename TI, typename TO, unsigned kVar>
+void launch_fwd_pers(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
+                     hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, true, cus, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr,
+                       g, nullptr, qp, 128.0f);
+}
+
 void launch_copy_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL(copy_tilepattern, dim3((g.ntiles + 255) / 256), dim3(256), 0, s, in, out, g);
 }
@@ -266,27 +274,32 @@ int main(int argc, char** argv) {
     constexpr unsigned B = L | N | F, R = kVarRowMajor, S = kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
     constexpr unsigned LL = kVarLdsLoad;
     constexpr unsigned NL = kVarNTLoad, IP = kVarI8Pack;
-    constexpr unsigned OR = kOctRestage;
+    constexpr unsigned PK = kVarPacked, OR = kOctRestage;
+    // u8 -> fp32 quantised (the headline kernel): each checked against "plain"
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
-        {"product (b512+lds+nt+fast)", launch_var<B | W512>},
-        {"octet u8 b256", launch_fwd_oct<uint8_t, float, F | N>},
-        {"octet u8 b256 restage", launch_fwd_oct<uint8_t, float, F | N | OR>},
-        {"octet u8 b512 restage", launch_fwd_oct<uint8_t, float, F | N | OR | W512>},
+        {"u8->f32 tile (product)", launch_var<B | W512>},
+        {"u8->f32 tile packed", launch_var<B | W512 | PK>},
+        {"u8->f32 octet", launch_fwd_oct<uint8_t, float, F | N | OR>},
     };
+    // pairs (2k, 2k+1), checked bit-exact against each other
     std::vector<Variant> other = {
-        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 duo b256", launch_fwd_duo<N>, true},
-        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 duo b512", launch_fwd_duo<N | W512>, true},
-        {"fwd f32 product", launch_fwd_any<float, float, L | N | W512>, true},
-        {"fwd f32 duo b256 plain-st", launch_fwd_duo<0>, true},
-        {"inv f32 octet (product)", launch_inv_oct<float, float, N | OR>, true},
-        {"inv f32 duo b256", launch_inv_duo<N>, true},
-        {"inv f32 octet (product)", launch_inv_oct<float, float, N | OR>, true},
-        {"inv f32 duo b512", launch_inv_duo<N | W512>, true},
-        {"compat fwd tile (product)", launch_fwd_compat_tile<L | N | W512>, true},
-        {"compat fwd duo b256", launch_fwd_compat_duo<N>, true},
+        {"fwd f32 tile", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32 duo", launch_fwd_duo<N>, true},
+        {"fwd f32 tile", launch_fwd_any<float, float, L | N | W512>, true},
+        {"fwd f32 octet", launch_fwd_oct<float, float, N | OR>, true},
+        {"inv f32 tile", launch_inv_any<float, float, L | N | W512>, true},
+        {"inv f32 duo", launch_inv_duo<N>, true},
+        {"inv f32 tile", launch_inv_any<float, float, L | N | W512>, true},
+        {"inv f32 octet", launch_inv_oct<float, float, N | OR>, true},
+        {"compat fwd tile", launch_fwd_compat_tile<L | N | W512>, true},
+        {"compat fwd duo", launch_fwd_compat_duo<N>, true},
+        {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
+        {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 octet", launch_fwd_oct<uint8_t, int8_t, F | N>},
+        {"inv i8->u8 tile", launch_inv_any<int8_t, uint8_t, N | W512>},
+        {"inv i8->u8 octet", launch_inv_oct<int8_t, uint8_t, N>},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
