@@ -26,12 +26,16 @@ namespace hpdct {
 
 namespace {
 
-constexpr uint32_t kDuoStride = 72;  // floats per tile in the slot (64 + pad)
-constexpr uint32_t kDuoTiles = 32;   // tiles per wave
+enum : unsigned {
+    kDuoTight = 1u << 21,  // unpadded slot (64 floats per tile): 8 KiB per wave, 5 waves/SIMD by LDS
+};
+constexpr uint32_t kDuoTiles = 32;  // tiles per wave
+template <unsigned kVar>
+constexpr uint32_t kDuoStride = (kVar & kDuoTight) ? 64u : 72u;  // floats per tile in the slot (64 + pad)
 
 template <unsigned kVar>
 __device__ __forceinline__ float* duo_slot() {
-    __shared__ __attribute__((aligned(16))) float xchg[kBlock<kVar> / 64u][kDuoTiles * kDuoStride];
+    __shared__ __attribute__((aligned(16))) float xchg[kBlock<kVar> / 64u][kDuoTiles * kDuoStride<kVar>];
     return xchg[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
 }
 
@@ -50,7 +54,7 @@ __device__ __forceinline__ void lds4(float* p, float a, float b, float c, float 
 template <unsigned kVar, typename Finish>
 __device__ __forceinline__ void duo_rows(float (&p)[8][4], float* slot_all, uint32_t t, uint32_t h,
                                          Finish&& finish, float (&o)[4][8]) {
-    float* const slot = slot_all + t * kDuoStride;
+    float* const slot = slot_all + t * kDuoStride<kVar>;
     unroll<8>([&](auto v) { lds4(slot + v * 8u + 4u * h, p[v][0], p[v][1], p[v][2], p[v][3]); });
     wave_lds_order();
     unroll<4>([&](auto k) {
@@ -69,7 +73,7 @@ __device__ __forceinline__ void duo_store(float* __restrict__ plane, const TileG
     constexpr bool kNT = (kVar & kVarNT) != 0;
     if (run) {
         const uint32_t lane = threadIdx.x & 63u;
-        float* const slot = slot_all + t * kDuoStride;
+        float* const slot = slot_all + t * kDuoStride<kVar>;
         unroll<4>([&](auto k) {
             const uint32_t r = 4u * h + k;
             lds4(slot + r * 8u, o[k][0], o[k][1], o[k][2], o[k][3]);
@@ -77,7 +81,7 @@ __device__ __forceinline__ void duo_store(float* __restrict__ plane, const TileG
         });
         wave_lds_order();
         // row k of the 32 tiles: lane l stores floats [4l, 4l+4) = tile l>>1, half l&1
-        const float* src = slot_all + (lane >> 1) * kDuoStride + 4u * (lane & 1u);
+        const float* src = slot_all + (lane >> 1) * kDuoStride<kVar> + 4u * (lane & 1u);
         unroll<8>([&](auto k) {
             st<kNT>(reinterpret_cast<float4*>(plane + run_base + k * g.width) + lane, ld4(src + k * 8u));
         });
@@ -101,7 +105,6 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
                                                                 const float* __restrict__ t_dev, QParams qp,
                                                                 float shift) {
     const TSource<kBuiltinT, false> T(t_dev);
-    const float* qtab = kQuant ? stage_tables<kVar, 1>(qp.q, nullptr) : nullptr;
     const uint32_t lane = threadIdx.x & 63u, t = lane >> 1, h = lane & 1u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t first = wave * kDuoTiles;
@@ -134,16 +137,17 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
         });
     });
     float o[4][8];
-    duo_rows<kVar>(pp, slot_all, t, h, [&](uint32_t r, auto, const float (&row)[8], float (&dst)[8]) {
+    duo_rows<kVar>(pp, slot_all, t, h, [&](uint32_t, auto k, const float (&row)[8], float (&dst)[8]) {
         unroll<8>([&](auto u) {
             float s = 0.0f;
             unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(row[i], s); });
             dst[u] = s;
         });
-        if constexpr (kQuant) {
-            const float4 q0 = ld4(qtab + r * 8u), q1 = ld4(qtab + r * 8u + 4u);
-            const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-            unroll<8>([&](auto u) { dst[u] = quantise<kVar>(dst[u], qv[u], 0.0f); });
+        if constexpr (kQuant) {  // row 4h+k of Q: two kernel-argument values, one select
+            unroll<8>([&](auto u) {
+                const float qv = h ? qp.q.v[(4 + k) * 8 + u] : qp.q.v[k * 8 + u];
+                dst[u] = quantise<kVar>(dst[u], qv, 0.0f);
+            });
         }
     }, o);
     duo_store<kVar>(out, g, run, run_base, p.base, p.valid, slot_all, t, h, o);
@@ -156,7 +160,6 @@ __global__ __launch_bounds__(kBlock<kVar>) void idct_duo_kernel(const float* __r
                                                                 const float* __restrict__ t_dev, Mat64 q,
                                                                 float shift) {
     const TSource<kBuiltinT, false> T(t_dev);
-    const float* qtab = kDequant ? stage_tables<kVar, 1>(q, nullptr) : nullptr;
     const uint32_t lane = threadIdx.x & 63u, t = lane >> 1, h = lane & 1u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t first = wave * kDuoTiles;
@@ -172,9 +175,8 @@ __global__ __launch_bounds__(kBlock<kVar>) void idct_duo_kernel(const float* __r
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (p.valid) v = ld4(coef + p.base + i * g.width + 4u * h);
         d[i][0] = v.x, d[i][1] = v.y, d[i][2] = v.z, d[i][3] = v.w;
-        if constexpr (kDequant) {
-            const float4 qq = ld4(qtab + i * 8u + 4u * h);
-            d[i][0] = d[i][0] * qq.x, d[i][1] = d[i][1] * qq.y, d[i][2] = d[i][2] * qq.z, d[i][3] = d[i][3] * qq.w;
+        if constexpr (kDequant) {  // columns 4h..4h+3 of Q row i: one select per value
+            unroll<4>([&](auto c) { d[i][c] = d[i][c] * (h ? q.v[i * 8 + 4 + c] : q.v[i * 8 + c]); });
         }
     });
     if constexpr (kDequant && (kVar & kVarWbDequant) != 0) {

@@ -207,6 +207,11 @@ void launch_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, const QPar
                        reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp, 128.0f);
 }
 template <unsigned kVar>
+void launch_fwd_duo_rt(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_duo_kernel<true, false, false, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, nullptr, g, g_T, qp, 128.0f);
+}
+template <unsigned kVar>
 void launch_inv_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL((idct_duo_kernel<true, true, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp.q, 128.0f);
@@ -288,6 +293,10 @@ int main(int argc, char** argv) {
         {"fwd f32 duo", launch_fwd_duo<N>, true},
         {"fwd f32 tile", launch_fwd_any<float, float, L | N | W512>, true},
         {"fwd f32 octet", launch_fwd_oct<float, float, N | OR>, true},
+        {"fwd f32 duo", launch_fwd_duo<N>, true},
+        {"fwd f32 duo runtime-T", launch_fwd_duo_rt<N>, true},
+        {"fwd f32 duo", launch_fwd_duo<N>, true},
+        {"fwd f32 duo tight", launch_fwd_duo<N | kDuoTight>, true},
         {"inv f32 tile", launch_inv_any<float, float, L | N | W512>, true},
         {"inv f32 duo", launch_inv_duo<N>, true},
         {"inv f32 tile", launch_inv_any<float, float, L | N | W512>, true},
