@@ -26,4 +26,7 @@ step bench 600 python bench.py "$@" || exit $?
 cd /tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o hpdct -- \
     python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-extras || exit $?
+# every kernel of the path (extras: fp32 duo/octet kernels, int8, baselines, C4, C5)
+step rocprof_full 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_full" -o hpdct -- \
+    python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --c5-frames 64 || exit $?
 echo ALLDONE

@@ -202,6 +202,12 @@ void launch_fwd_compat_duo(const uint8_t* in, float* out, const TileGrid& g, con
                        reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
 }
 template <unsigned kVar>
+void launch_fwd_compat_oct(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((fdct_octet_kernel<float, float, true, false, true, kVar>), octet_grid(g, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
+}
+template <unsigned kVar>
 void launch_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL((fdct_duo_kernel<true, true, false, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const float*>(in), out, nullptr, g, nullptr, qp, 128.0f);
@@ -303,6 +309,8 @@ int main(int argc, char** argv) {
         {"inv f32 octet", launch_inv_oct<float, float, N | OR>, true},
         {"compat fwd tile", launch_fwd_compat_tile<L | N | W512>, true},
         {"compat fwd duo", launch_fwd_compat_duo<N>, true},
+        {"compat fwd tile", launch_fwd_compat_tile<L | N | W512>, true},
+        {"compat fwd octet", launch_fwd_compat_oct<N | OR>, true},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
         {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
