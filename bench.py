@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--c4-size", type=int, default=16384)
     ap.add_argument("--c5-size", type=int, default=4096)
     ap.add_argument("--c5-frames", type=int, default=512)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank flow with several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -64,14 +67,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU: LOCAL_RANK is the device (modulo the visible devices,
+    # so a gloo rehearsal can put several ranks on one GPU)
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if ndev else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         # collectives raise (instead of aborting the process) if a peer dies, so
         # rank 0 can still print the headline line; generous timeout
         os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
         import datetime
-        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=240))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=240))
+        else:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=240))
 
     def barrier():
         if world > 1:
@@ -80,7 +90,7 @@ def main():
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -392,6 +402,20 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
             hpdct.fill_hash_u8(xf, seed=42, first_index=0)
             ref = hpdct.forward(xf)
             out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
+            # the same full frame on this one GPU: the compute-phase node speedup
+            # (BASELINE.md C4 target >= 6x at 8 GPUs)
+            fcall = hpdct.bind("fwd", xf, ref, stream=stream)
+            for _ in range(3):
+                fcall()
+            fa, fb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fa.record(stream)
+            for _ in range(reps):
+                fcall()
+            fb.record(stream)
+            torch.cuda.synchronize()
+            one_gpu_ms = fa.elapsed_time(fb) / reps
+            out["one_gpu_full_frame_ms"] = round(one_gpu_ms, 4)
+            out["compute_speedup_vs_1gpu"] = round(one_gpu_ms / compute_ms, 2)
             del xf, ref, full
     del x, y
     torch.cuda.empty_cache()

@@ -37,10 +37,16 @@ def gather_slabs(local, height: int, width: int, root: int = 0, group=None):
     full (height x width) tensor on `root`; returns it there, None elsewhere.
 
     Uses torch.distributed.gather when all slabs have the same size (the
-    common case: height divisible by 8*world), else a send/recv fan-in."""
+    common case: height divisible by 8*world), else a send/recv fan-in.
+    With the gloo backend, device tensors are staged through host memory
+    (gloo's gather and point-to-point take host tensors); RCCL moves them
+    device to device over xGMI."""
     import torch
     import torch.distributed as dist
 
+    if local.device.type != "cpu" and dist.get_backend(group) == "gloo":
+        full = gather_slabs(local.cpu(), height, width, root, group)
+        return None if full is None else full.to(local.device)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     shards = all_shards(height, world)
