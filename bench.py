@@ -275,6 +275,13 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         hpdct.forward(imgs[0], outs[0])
         r = hpdct.inverse(outs[0], rec[0])
         r8 = hpdct.inverse(outs[0], out_dtype=torch.uint8)  # clamp + truncate (utils.cu:18-24)
+        # C3 round trip timed: forward u8 -> fp32 coefficients, inverse -> u8 pixels
+        rt_px = [torch.empty((n, n), dtype=torch.uint8, device=dev) for _ in range(2)]
+        fwd = [hpdct.bind("fwd", imgs[s], outs[s], stream=stream) for s in range(args.sets)]
+        inv = [hpdct.bind("inv", outs[s], rt_px[s % 2], stream=stream) for s in range(args.sets)]
+        pair = [lambda s=s: (fwd[s](), inv[s]()) for s in range(args.sets)]
+        rms, _, _ = timed_loop(pair, steps, 4)
+        rt_ms = rms / steps
         x = imgs[0].double()
         sx = float((x * x).sum())
         se = float(((x - r.double()) ** 2).sum())
@@ -282,8 +289,10 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         extras["c3_roundtrip"] = {
             "mse_f32": se / px, "peen_f32_pct": 100.0 * (se / sx) ** 0.5,
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
+            "ms_per_frame_fwd_inv_u8": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
+            "bytes_per_px": 10,
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
-        del f32_in, i8, rec, r8, x
+        del f32_in, i8, rec, r8, x, rt_px
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024

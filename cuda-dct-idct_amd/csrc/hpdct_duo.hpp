@@ -205,6 +205,139 @@ __global__ __launch_bounds__(kBlock<kVar>) void idct_duo_kernel(const float* __r
     duo_store<kVar>(out, g, run, run_base, p.base, p.valid, slot_all, t, h, o);
 }
 
+// cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST), duo mapping, fp32 -> fp32.
+//   forward  R = X.T^T (row chains, main_cublass_2.cu:228-231), C = T.R (column
+//            chains, :232-235), round(C / Q); X - 128 optionally written back.
+//   inverse  D = q*Q (optionally written back, :285), R = D.T (row chains,
+//            :288-291), out = T^T.R + 128 (column chains, :292-295).
+// The first chain runs along a row, so lanes own rows first: the 8 rows of the
+// wave's 32 tiles arrive as 1 KiB-contiguous loads staged through LDS (the
+// write-back leaves from the same registers, 1 KiB-contiguous), lane (t, h)
+// takes rows 4h..4h+3 and runs the row chains; R goes back to LDS transposed and
+// the lane takes columns 4h..4h+3 for the column chains; the results are staged
+// once more for 1 KiB-contiguous stores.  Chains, division and rounding as
+// fdct_tile_rowfirst / idct_tile_rowfirst: bit-identical to the tile kernel.
+template <bool kInv, bool kQ, bool kBuiltinT, bool kWb, unsigned kVar>
+__global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float* __restrict__ src,
+                                                                    float* __restrict__ out, float* __restrict__ wb,
+                                                                    TileGrid g, const float* __restrict__ t_dev,
+                                                                    Mat64 q, float shift) {
+    constexpr bool kNT = (kVar & kVarNT) != 0;
+    constexpr uint32_t S = kDuoStride<kVar>;
+    const TSource<kBuiltinT, false> T(t_dev);
+    const uint32_t lane = threadIdx.x & 63u, t = lane >> 1, h = lane & 1u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
+    const uint32_t first = wave * kDuoTiles;
+    if (first >= g.ntiles) return;
+    const OctetPos p = octet_pos(g, first + t);
+    const bool run = duo_run(g, first);
+    const uint64_t run_base = octet_pos(g, first).base;
+    float* const slot_all = duo_slot<kVar>();
+    float* const slot = slot_all + t * S;
+
+    // input element (row, col) prepared as the reference's first kernel leaves
+    // it: X - 128 (forward) or q * Q (inverse, dequantised)
+    auto prep = [&](float v, float qv) {
+        if constexpr (kInv) {
+            return kQ ? v * qv : v;
+        } else {
+            (void)qv;
+            return v - shift;
+        }
+    };
+    float x[4][8];  // rows 4h..4h+3 of the lane's tile
+    if (run) {
+        // row k of the 32 tiles: lane l holds floats [4l, 4l+4) = tile l>>1, columns 4(l&1)..+3
+        const uint32_t hh = lane & 1u;
+        unroll<8>([&](auto k) {
+            const float4 v = ld4(src + run_base + k * g.width + 4u * lane);
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            float e[4];
+            unroll<4>([&](auto c) {
+                const float qv = kInv && kQ ? (hh ? q.v[k * 8 + 4 + c] : q.v[k * 8 + c]) : 0.0f;
+                e[c] = prep(vv[c], qv);
+            });
+            if constexpr (kWb)
+                st<kNT>(reinterpret_cast<float4*>(wb + run_base + k * g.width) + lane, make_float4(e[0], e[1], e[2], e[3]));
+            lds4(slot_all + (lane >> 1) * S + k * 8u + 4u * hh, e[0], e[1], e[2], e[3]);
+        });
+        wave_lds_order();
+        unroll<4>([&](auto k) {
+            const float4 a = ld4(slot + (4u * h + k) * 8u), b = ld4(slot + (4u * h + k) * 8u + 4u);
+            x[k][0] = a.x, x[k][1] = a.y, x[k][2] = a.z, x[k][3] = a.w;
+            x[k][4] = b.x, x[k][5] = b.y, x[k][6] = b.z, x[k][7] = b.w;
+        });
+    } else {
+        unroll<4>([&](auto k) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+            if (p.valid) {
+                a = ld4(src + p.base + (4u * h + k) * g.width);
+                b = ld4(src + p.base + (4u * h + k) * g.width + 4u);
+            }
+            const float raw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            unroll<8>([&](auto j) {
+                const float qv = kInv && kQ ? (h ? q.v[(4 + k) * 8 + j] : q.v[k * 8 + j]) : 0.0f;
+                x[k][j] = prep(raw[j], qv);
+            });
+            if constexpr (kWb) {
+                if (p.valid) {
+                    float4* dst = reinterpret_cast<float4*>(wb + p.base + (4u * h + k) * g.width);
+                    st<kNT>(dst, make_float4(x[k][0], x[k][1], x[k][2], x[k][3]));
+                    st<kNT>(dst + 1, make_float4(x[k][4], x[k][5], x[k][6], x[k][7]));
+                }
+            }
+        });
+    }
+    // row chains: R[i][u] = sum_j x[i][j] T[u][j] (forward) / sum_j x[i][j] T[j][u] (inverse)
+    float r[4][8];
+    unroll<4>([&](auto k) {
+        unroll<8>([&](auto u) {
+            float s = 0.0f;
+            unroll<8>([&](auto j) { s = T.template mac<kInv ? j * 8 + u : u * 8 + j>(x[k][j], s); });
+            r[k][u] = s;
+        });
+    });
+    // R transposed into the slot: column u of the tile at [u*8 .. u*8+8)
+    wave_lds_order();
+    unroll<8>([&](auto u) { lds4(slot + u * 8u + 4u * h, r[0][u], r[1][u], r[2][u], r[3][u]); });
+    wave_lds_order();
+    float col[4][8];  // columns 4h..4h+3 of R
+    unroll<4>([&](auto c) {
+        const float4 a = ld4(slot + (4u * h + c) * 8u), b = ld4(slot + (4u * h + c) * 8u + 4u);
+        col[c][0] = a.x, col[c][1] = a.y, col[c][2] = a.z, col[c][3] = a.w;
+        col[c][4] = b.x, col[c][5] = b.y, col[c][6] = b.z, col[c][7] = b.w;
+    });
+    // column chains: C[v][u] = sum_i T[v][i] R[i][u] (forward) / sum_i T[i][v] R[i][u] (inverse)
+    float o[4][8];  // o[c][v] = output (v, 4h+c)
+    unroll<4>([&](auto c) {
+        unroll<8>([&](auto v) {
+            float s = 0.0f;
+            unroll<8>([&](auto i) { s = T.template mac<kInv ? i * 8 + v : v * 8 + i>(col[c][i], s); });
+            if constexpr (kInv) {
+                s = s + shift;  // add_matrix_scalar, no clamp
+            } else if constexpr (kQ) {
+                const float qv = h ? q.v[v * 8 + 4 + c] : q.v[v * 8 + c];
+                s = quantise<kVar>(s, qv, 0.0f);
+            }
+            o[c][v] = s;
+        });
+    });
+    wave_lds_order();
+    if (run) {
+        unroll<8>([&](auto v) { lds4(slot + v * 8u + 4u * h, o[0][v], o[1][v], o[2][v], o[3][v]); });
+        wave_lds_order();
+        const float* from = slot_all + (lane >> 1) * S + 4u * (lane & 1u);
+        unroll<8>([&](auto k) {
+            st<kNT>(reinterpret_cast<float4*>(out + run_base + k * g.width) + lane, ld4(from + k * 8u));
+        });
+    } else if (p.valid) {
+        unroll<8>([&](auto v) {
+            st<kNT>(reinterpret_cast<float4*>(out + p.base + v * g.width + 4u * h),
+                    make_float4(o[0][v], o[1][v], o[2][v], o[3][v]));
+        });
+    }
+}
+
 inline dim3 duo_grid(const TileGrid& g, uint32_t block) {
     const uint32_t waves = (g.ntiles + kDuoTiles - 1u) / kDuoTiles;
     const uint32_t per = block / 64u;

@@ -108,6 +108,14 @@ hipError_t idct_duo_go(const float* coef, float* out, float* dq_out, const TileG
     return hipGetLastError();
 }
 
+template <unsigned kV, bool kInv, bool kQ, bool kBuiltinT, bool kWb>
+hipError_t rowfirst_duo_go(const float* src, float* out, float* wb, const TileGrid& g, const float* t_dev,
+                           const Mat64& q, float shift, hipStream_t s) {
+    hipLaunchKernelGGL((rowfirst_duo_kernel<kInv, kQ, kBuiltinT, kWb, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>),
+                       0, s, src, out, wb, g, t_dev, q, shift);
+    return hipGetLastError();
+}
+
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                             const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
@@ -115,9 +123,13 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
     constexpr unsigned kOct = kOctVar<TOut>;
     constexpr bool kFastDivOk = std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback;
     if constexpr (std::is_same_v<TIn, float> && std::is_same_v<TOut, float>) {
-        if (row_first)  // cublasDCTv2 pass order: tile-per-lane only
+        if (row_first) {  // cublasDCTv2 pass order: duo (rows first), or tile when forced
+            if (mapping_mode() != HPDCT_MAPPING_TILE)
+                return rowfirst_duo_go<kDuoVar, false, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
+                                                                                      q.q, shift, s);
             return fdct_go<kBase | kVarRowFirst, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
                                                                                            t_dev, q, shift, s);
+        }
     }
     (void)row_first;
     constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
@@ -167,7 +179,16 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
     constexpr unsigned kOct = kOctVar<TOut>;
     constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
     if constexpr (kF32) {
-        if (row_first) {  // cublasDCTv2 pass order: tile-per-lane only
+        if (row_first) {  // cublasDCTv2 pass order: duo (rows first), or tile when forced
+            if (mapping_mode() != HPDCT_MAPPING_TILE) {
+                if constexpr (kDequant) {
+                    if (dq_out)
+                        return rowfirst_duo_go<kDuoVar, true, kDequant, kBuiltinT, true>(coef, out, dq_out, g, t_dev,
+                                                                                         q, shift, s);
+                }
+                return rowfirst_duo_go<kDuoVar, true, kDequant, kBuiltinT, false>(coef, out, nullptr, g, t_dev, q,
+                                                                                  shift, s);
+            }
             if constexpr (kDequant) {
                 if (dq_out)
                     return idct_go<kV | kVarRowFirst | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(

@@ -147,8 +147,8 @@ hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_
  *          fp32 -> fp32, one lane per tile for the rest (DESIGN.md "Kernels").
  *   TILE   one lane per tile always.     OCTET  eight lanes per tile always.
  *   DUO    two lanes per tile for every fp32 -> fp32 kernel, AUTO otherwise.
- * The cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST) always runs one lane per
- * tile.  Process-wide; the initial value comes from the environment variable
+ * The cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST) runs two lanes per tile
+ * (rows first) except under TILE.  Process-wide; the initial value comes from the environment variable
  * HPDCT_MAPPING ("auto", "tile", "octet", "duo"), else AUTO.  For A/B
  * measurement and tests; set it while no call is in flight. */
 typedef enum hpdct_mapping {

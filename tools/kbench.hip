@@ -207,6 +207,33 @@ void launch_fwd_compat_oct(const uint8_t* in, float* out, const TileGrid& g, con
     hipLaunchKernelGGL((fdct_octet_kernel<float, float, true, false, true, kVar>), octet_grid(g, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
 }
+// cublasDCTv2 order: runtime T, X-128 / q*Q written back (to the scratch plane)
+template <unsigned kVar>
+void launch_cublas_fwd_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                            hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<float, float, true, false, true, kVar | kVarRowFirst>),
+                       grid_for(g, false, 0, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
+}
+template <unsigned kVar>
+void launch_cublas_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((rowfirst_duo_kernel<false, true, false, true, kVar>), duo_grid(g, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp.q, 128.0f);
+}
+template <unsigned kVar>
+void launch_cublas_inv_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                            hipStream_t s) {
+    hipLaunchKernelGGL((idct_kernel<float, float, true, false, kVar | kVarRowFirst | kVarWbDequant>),
+                       grid_for(g, false, 0, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp.q, 128.0f);
+}
+template <unsigned kVar>
+void launch_cublas_inv_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((rowfirst_duo_kernel<true, true, false, true, kVar>), duo_grid(g, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp.q, 128.0f);
+}
 template <unsigned kVar>
 void launch_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL((fdct_duo_kernel<true, true, false, kVar>), duo_grid(g, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
@@ -311,6 +338,10 @@ int main(int argc, char** argv) {
         {"compat fwd duo", launch_fwd_compat_duo<N>, true},
         {"compat fwd tile", launch_fwd_compat_tile<L | N | W512>, true},
         {"compat fwd octet", launch_fwd_compat_oct<N | OR>, true},
+        {"cublas fwd tile", launch_cublas_fwd_tile<L | N | W512>, true},
+        {"cublas fwd duo", launch_cublas_fwd_duo<N>, true},
+        {"cublas inv tile", launch_cublas_inv_tile<L | N | W512>, true},
+        {"cublas inv duo", launch_cublas_inv_duo<N>, true},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
         {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
