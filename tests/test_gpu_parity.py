@@ -428,3 +428,36 @@ def test_c3_8192_roundtrip(hp, oracle, dev, golden):
     import torch
     assert float((rt - x.float()).abs().max()) < 1e-4
     assert float(qd.abs().max()) <= 98
+
+
+# --------------------------------------------------------------------- beyond 32-bit indexing
+@pytest.mark.parametrize("out", ["f32", "i8"])
+def test_beyond_int32_pixel_count(hp, oracle, dev, out):
+    """A 32776 x 65536 frame (2^31 + 2^19 pixels): the reference's int indices
+    overflow here; every offset in the kernels is 64-bit.  The
+    frame is generated on the device by the stateless hash, so the oracle can
+    regenerate any 8-row slab; tiles are independent, so crops of the output
+    are checked against the oracle on the same crops of the input (top, middle
+    and bottom slabs, left and right edges), forward and (fp32) inverse."""
+    import torch
+    h, w, seed = 32776, 65536, 7
+    x = torch.empty((h, w), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=seed)
+    y = hp.forward(x, out_dtype=torch.float32 if out == "f32" else torch.int8)
+    r = hp.inverse(y) if out == "f32" else None
+    torch.cuda.synchronize()
+    try:
+        for r0 in (0, (h // 16) * 8, h - 8):
+            slab = oracle.hash_u8(8 * w, seed=seed, first_index=r0 * w).reshape(8, w)
+            for c0 in (0, w - 1024):
+                crop = np.ascontiguousarray(slab[:, c0:c0 + 1024])
+                q_ref = oracle.fdct(crop)
+                got = y[r0:r0 + 8, c0:c0 + 1024].cpu().numpy()
+                if out == "f32":
+                    assert bits_equal(got, q_ref), (r0, c0)
+                    assert bits_equal(r[r0:r0 + 8, c0:c0 + 1024].cpu().numpy(), oracle.idct(q_ref)), (r0, c0)
+                else:
+                    assert np.array_equal(got.astype(np.float32), q_ref), (r0, c0)
+    finally:
+        del x, y, r
+        torch.cuda.empty_cache()

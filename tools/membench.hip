@@ -85,6 +85,28 @@ __global__ __launch_bounds__(256) void copy_f32(const float4* __restrict__ in, f
     }
 }
 
+// 1 B in / 1 B out (the int8 forward's traffic mix): grid-stride copy of
+// 8-byte (uint2) or 16-byte (uint4) lane pieces
+template <typename V, bool kNT>
+__global__ __launch_bounds__(256) void copy_bytes(const V* __restrict__ in, V* __restrict__ out, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) {
+        const V v = in[i];
+        if constexpr (kNT) {
+            if constexpr (sizeof(V) == 8) {
+                __builtin_nontemporal_store(v.x, &out[i].x);
+                __builtin_nontemporal_store(v.y, &out[i].y);
+            } else {
+                __builtin_nontemporal_store(v.x, &out[i].x);
+                __builtin_nontemporal_store(v.y, &out[i].y);
+                __builtin_nontemporal_store(v.z, &out[i].z);
+                __builtin_nontemporal_store(v.w, &out[i].w);
+            }
+        } else {
+            out[i] = v;
+        }
+    }
+}
+
 template <bool kNT>
 __global__ __launch_bounds__(256) void write_only(float4* __restrict__ out, uint64_t n4) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -244,11 +266,36 @@ int main(int argc, char** argv) {
                                                 sink);
                          }});
     }
+    for (int gm : {4, 8, 16}) {
+        const unsigned grid = cus * gm;
+        cases.push_back({"copy_u8 x8 plain g" + std::to_string(gm), 2.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((copy_bytes<uint2, false>), dim3(grid), dim3(256), 0, 0,
+                                                (const uint2*)in[s], (uint2*)out[s], (uint64_t)px / 8);
+                         }});
+        cases.push_back({"copy_u8 x8 nt    g" + std::to_string(gm), 2.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((copy_bytes<uint2, true>), dim3(grid), dim3(256), 0, 0,
+                                                (const uint2*)in[s], (uint2*)out[s], (uint64_t)px / 8);
+                         }});
+        cases.push_back({"copy_u8 x16 nt   g" + std::to_string(gm), 2.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((copy_bytes<uint4, true>), dim3(grid), dim3(256), 0, 0,
+                                                (const uint4*)in[s], (uint4*)out[s], (uint64_t)px / 16);
+                         }});
+    }
+    cases.push_back({"hipMemcpyD2D 1B/px (r+w)", 2.0 * px, [=](int s) {
+                         CK(hipMemcpyAsync(out[s], in[(s + 1) % nsets], px, hipMemcpyDeviceToDevice, 0));
+                     }});
     cases.push_back({"hipMemcpyD2D 4B/px (r+w)", 8.0 * px, [=](int s) {
                          CK(hipMemcpyAsync(out[s], out[(s + 1) % nsets], px * 4, hipMemcpyDeviceToDevice, 0));
                      }});
     cases.push_back({"hipMemsetD32 4B/px", 4.0 * px, [=](int s) { CK(hipMemsetD32Async((hipDeviceptr_t)out[s], 7, px, 0)); }});
 
+    if (argc > 3 && strcmp(argv[3], "u8") == 0) {
+        std::vector<Case> keep;
+        for (auto& c : cases)
+            if (c.name.find("copy_u8") != std::string::npos || c.name.find("1B/px") != std::string::npos)
+                keep.push_back(c);
+        cases.swap(keep);
+    }
     if (argc > 3 && strcmp(argv[3], "f32") == 0) {
         std::vector<Case> keep;
         for (auto& c : cases)
