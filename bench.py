@@ -493,7 +493,7 @@ def _cpu_baseline(n):
     mt_med = float(np.median(mt))
     return {"value": round(n * n / med / 1e9, 5), "unit": "Gpixel/s", "cores": 1, "kind": "port",
             "sample": f"full {n}x{n} frame (srand(42) rand()%256), forward DCT + quantise, median of 3 runs "
-                      f"({med:.3f} s each), 1 thread, gcc -O2 -ffp-contract=off",
+                      f"({med:.3f} s each), 1 thread, gcc -O3 -ffp-contract=off",
             "ms_per_frame": round(med * 1e3, 1), "host_cpu": model, "host_nproc": os.cpu_count(),
             "all_cores": {"value": round(n * n / mt_med / 1e9, 5), "unit": "Gpixel/s", "cores": threads,
                           "ms_per_frame": round(mt_med * 1e3, 1),

@@ -31,7 +31,7 @@
  *   - utils.cu:10-15 / :18-24      convertToFloat / convertToUnsignedChar
  *   - main_newAppr.cu:60-81        the Q table and the T matrix
  *
- * Build: gcc -O2 -ffp-contract=off (oracle/Makefile).  Contraction MUST stay
+ * Build: gcc -O3 -ffp-contract=off (oracle/Makefile).  Contraction MUST stay
  * off: every fused multiply-add below is an explicit fmaf().
  */
 #include <math.h>
