@@ -47,6 +47,9 @@ enum : unsigned {
     kVarNTLoad = 1u << 16,    // non-temporal loads of the 8-bit input planes
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
+    kVarPersist2 = 1u << 22,    // persistent waves, next set prefetched under a wave-uniform branch only
+                                // (per-lane addresses clamped instead of divergent loads), so the
+                                // compute of set n overlaps the loads of set n+1
     kVarPacked = 1u << 19,      // uint8 input, built-in T, quantised: packed-fp32 transform and quotient
                                 // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, fdct_tile_pk)
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
@@ -177,6 +180,11 @@ struct RawTile;
 template <>
 struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
     uint2 r[8];
+    // an empty asm that consumes every register: the loads must have landed
+    // here (persistent walk: keeps the wait out of the pipelined loop)
+    __device__ __forceinline__ void settle() {
+        unroll<8>([&](auto i) { asm volatile("" : "+v"(r[i].x), "+v"(r[i].y)); });
+    }
     __device__ __forceinline__ void load(const uint8_t* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
     }
@@ -210,6 +218,9 @@ struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
 template <>
 struct RawTile<int8_t> {  // int8 coefficients, 16 VGPRs
     uint2 r[8];
+    __device__ __forceinline__ void settle() {
+        unroll<8>([&](auto i) { asm volatile("" : "+v"(r[i].x), "+v"(r[i].y)); });
+    }
     __device__ __forceinline__ void load(const int8_t* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
     }
@@ -224,7 +235,13 @@ struct RawTile<int8_t> {  // int8 coefficients, 16 VGPRs
 };
 
 template <>
-struct RawTile<float> {  // 64 VGPRs
+struct RawTile<float> {
+    __device__ __forceinline__ void settle() {
+        unroll<16>([&](auto n) {
+            float4& v = r[n / 2][n % 2];
+            asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+        });
+    }  // 64 VGPRs
     float4 r[8][2];
     __device__ __forceinline__ void load(const float* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) {
@@ -342,7 +359,38 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         seg = p.base - 8u * static_cast<uint64_t>(lane);
         return ok;
     };
-    if constexpr (!kPersist) {
+    if constexpr ((kVar & kVarPersist2) != 0) {
+        const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
+        uint32_t set = wave;
+        if (set >= nsets) return;
+        auto load_set = [&](RawTile<TIn>& r, uint32_t s_) {
+            uint32_t t = s_ * 64u + lane;
+            if (t >= g.ntiles) t = g.ntiles - 1u;  // clamp: every lane loads, no divergent load
+            r.load(src + tile_pos(g, t).base, g.width);
+        };
+        RawTile<TIn> cur;
+        load_set(cur, set);
+        cur.settle();  // first set waited here, once: no load of it is pending at the loop header
+        while (true) {
+            const uint32_t nset = set + nwaves;
+            const bool more = nset < nsets;  // wave-uniform
+            RawTile<TIn> nxt;
+            if (more) load_set(nxt, nset);
+            // lanes past the last tile run the body on their clamped tile (the
+            // last valid one): they store byte-identical values to the same
+            // addresses, so the loop body has no divergent branch and the
+            // wait for the next set's loads does not have to drain the stores
+            uint32_t t = set * 64u + lane;
+            if (t >= g.ntiles) t = g.ntiles - 1u;
+            const TilePos p = tile_pos(g, t);
+            uint64_t seg;
+            const bool ok = seg_info(set, p, seg);
+            body(cur, p, ok, seg);
+            if (!more) break;
+            cur = nxt;
+            set = nset;
+        }
+    } else if constexpr (!kPersist) {
         if (wave >= nsets) return;
         const TilePos p = tile_pos(g, wave * 64u + lane);
         uint64_t seg;

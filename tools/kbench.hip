@@ -258,6 +258,41 @@ void launch_fwd_pers(const uint8_t* in, float* out, const TileGrid& g, const QPa
                        g, nullptr, qp, 128.0f);
 }
 
+// the int8 forward's exact access pattern with no arithmetic: one lane per
+// tile, 8 rows x 8 B loaded, the same 8 rows x 8 B stored (NT), 512-thread
+// workgroups, one 64-tile set per wave
+__global__ __launch_bounds__(512) void pattern_copy_u8(const uint8_t* __restrict__ in, int8_t* __restrict__ out,
+                                                       TileGrid g) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 8u + threadIdx.x / 64u;
+    const uint32_t tile = wave * 64u + lane;
+    if (tile >= g.ntiles) return;
+    const uint32_t by = tile / g.tiles_x, bx = tile - by * g.tiles_x;
+    const uint64_t base = (uint64_t)by * 8u * g.width + (uint64_t)bx * 8u;
+    uint2 r[8];
+    for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint2*>(in + base + i * g.width);
+    for (int i = 0; i < 8; ++i) {
+        uint2* d = reinterpret_cast<uint2*>(out + base + i * g.width);
+        __builtin_nontemporal_store(r[i].x ^ 0x80808080u, &d->x);
+        __builtin_nontemporal_store(r[i].y ^ 0x80808080u, &d->y);
+    }
+}
+void launch_pattern_copy(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
+    hipLaunchKernelGGL(pattern_copy_u8, dim3((g.ntiles / 64 + 7) / 8), dim3(512), 0, s, in,
+                       reinterpret_cast<int8_t*>(out), g);
+}
+
+// persistent int8 forward with next-set prefetch, kW waves per CU
+template <unsigned kVar, uint32_t kW>
+void launch_i8_pers_w(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
+                      hipStream_t s) {
+    const uint32_t per = kBlock<kVar> / 64u;
+    const uint32_t sets = (g.ntiles + 63u) / 64u;
+    const uint32_t blocks = std::min<uint32_t>((sets + per - 1) / per, cus * kW / per);
+    hipLaunchKernelGGL((fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(blocks), dim3(kBlock<kVar>), 0,
+                       s, in, reinterpret_cast<int8_t*>(out), nullptr, g, nullptr, qp, 128.0f);
+}
+
 void launch_copy_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL(copy_tilepattern, dim3((g.ntiles + 255) / 256), dim3(256), 0, s, in, out, g);
 }
@@ -342,6 +377,12 @@ int main(int argc, char** argv) {
         {"cublas fwd duo", launch_cublas_fwd_duo<N>, true},
         {"cublas inv tile", launch_cublas_inv_tile<L | N | W512>, true},
         {"cublas inv duo", launch_cublas_inv_duo<N>, true},
+        {"pattern copy u8->i8 (no math)", launch_pattern_copy},
+        {"pattern copy u8->i8 (no math)", launch_pattern_copy},
+        {"fwd u8->i8 pers2 w16", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 16>},
+        {"fwd u8->i8 pers2 w20", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 20>},
+        {"fwd u8->i8 pers2 w8", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 8>},
+        {"fwd u8->i8 pers2 w12", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 12>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
         {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
