@@ -146,11 +146,38 @@ def test_quant_table_paths(hp, oracle, dev, c1, qtab):
     assert bits_equal(got_nq, oracle.fdct(np.full((16, 16), 255, np.uint8), Q=Q))
 
 
-@pytest.mark.parametrize("h,w", [(8, 8), (8, 16), (16, 8), (24, 40), (8, 4096), (520, 8), (1000, 1008), (72, 2056)])
+SHAPES = [(8, 8), (8, 16), (16, 8), (24, 40), (8, 4096), (520, 8), (1000, 1008), (72, 2056)]
+
+
+@pytest.mark.parametrize("h,w", SHAPES)
 def test_forward_shapes(hp, oracle, dev, h, w):
     img = np.random.default_rng(h * 7919 + w).integers(0, 256, (h, w), dtype=np.uint8)
     assert bits_equal(to_host(hp.forward(to_dev(img, dev))), oracle.fdct(img))
     assert bits_equal(to_host(hp.forward(to_dev(img.astype(np.float32), dev))), oracle.fdct(img))
+
+
+@pytest.mark.parametrize("h,w", SHAPES)
+def test_fp32_paths_shapes(hp, oracle, dev, h, w):
+    """Every fp32 -> fp32 kernel at ragged shapes (partial waves, tile rows
+    narrower than a wave's tiles, waves straddling tile rows): the inverse, the
+    forward with the X-128 write-back, and the cublasDCTv2 order both ways
+    with its write-backs (row-first duo kernel unless the mapping is TILE)."""
+    img = np.random.default_rng(h * 31 + w).integers(0, 256, (h, w)).astype(np.float32)
+    q = oracle.fdct(img)
+    assert bits_equal(to_host(hp.inverse(to_dev(q, dev))), oracle.idct(q))
+    x = to_dev(img, dev)
+    got = to_host(hp.forward(x, writeback_shift=True))
+    assert bits_equal(got, q)
+    assert bits_equal(to_host(x), img - 128.0)
+    x = to_dev(img, dev)
+    qr = to_host(hp.forward(x, row_first=True, writeback_shift=True))
+    assert bits_equal(qr, oracle.fdct(img, row_first=True))
+    assert bits_equal(to_host(x), img - 128.0)
+    qd = to_dev(qr, dev)
+    rr = to_host(hp.inverse(qd, row_first=True, writeback_dequant=True))
+    assert bits_equal(rr, oracle.idct(qr, row_first=True))
+    qtab = np.tile(oracle.default_quant(), (h // 8, w // 8))
+    assert bits_equal(to_host(qd), qr * qtab)
 
 
 def test_forward_extremes(hp, oracle, dev):
