@@ -50,6 +50,8 @@ enum : unsigned {
     kVarPersist2 = 1u << 22,    // persistent waves, next set prefetched under a wave-uniform branch only
                                 // (per-lane addresses clamped instead of divergent loads), so the
                                 // compute of set n overlaps the loads of set n+1
+    kVarTwoSets = 1u << 23,     // each wave takes two consecutive sets, all 16 row loads issued up front:
+                                // the first set's compute overlaps the second set's loads
     kVarPacked = 1u << 19,      // uint8 input, built-in T, quantised: packed-fp32 transform and quotient
                                 // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, fdct_tile_pk)
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
@@ -359,7 +361,25 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         seg = p.base - 8u * static_cast<uint64_t>(lane);
         return ok;
     };
-    if constexpr ((kVar & kVarPersist2) != 0) {
+    if constexpr ((kVar & kVarTwoSets) != 0) {
+        const uint32_t s0 = wave * 2u;
+        if (s0 >= nsets) return;
+        auto clamp_tile = [&](uint32_t s_) {
+            uint32_t t = s_ * 64u + lane;
+            return t < g.ntiles ? t : g.ntiles - 1u;  // lanes past the end redo the last tile (same bytes)
+        };
+        RawTile<TIn> a, b;
+        const TilePos pa = tile_pos(g, clamp_tile(s0)), pb = tile_pos(g, clamp_tile(s0 + 1u));
+        a.load(src + pa.base, g.width);
+        b.load(src + pb.base, g.width);
+        uint64_t seg;
+        bool ok = seg_info(s0, pa, seg);
+        body(a, pa, ok, seg);
+        if (s0 + 1u < nsets) {  // wave-uniform
+            ok = seg_info(s0 + 1u, pb, seg);
+            body(b, pb, ok, seg);
+        }
+    } else if constexpr ((kVar & kVarPersist2) != 0) {
         const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
         uint32_t set = wave;
         if (set >= nsets) return;

@@ -293,6 +293,19 @@ void launch_i8_pers_w(const uint8_t* in, float* out, const TileGrid& g, const QP
                        s, in, reinterpret_cast<int8_t*>(out), nullptr, g, nullptr, qp, 128.0f);
 }
 
+template <unsigned kVar>
+void launch_i8_two(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
+    hipLaunchKernelGGL((fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
+                       dim3(kBlock<kVar>), 0, s, in, reinterpret_cast<int8_t*>(out), nullptr, g, nullptr, qp, 128.0f);
+}
+template <unsigned kVar>
+void launch_f32_two(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
+    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
+                       dim3(kBlock<kVar>), 0, s, in, out, nullptr, g, nullptr, qp, 128.0f);
+}
+
 void launch_copy_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams&, uint32_t, hipStream_t s) {
     hipLaunchKernelGGL(copy_tilepattern, dim3((g.ntiles + 255) / 256), dim3(256), 0, s, in, out, g);
 }
@@ -379,10 +392,12 @@ int main(int argc, char** argv) {
         {"cublas inv duo", launch_cublas_inv_duo<N>, true},
         {"pattern copy u8->i8 (no math)", launch_pattern_copy},
         {"pattern copy u8->i8 (no math)", launch_pattern_copy},
-        {"fwd u8->i8 pers2 w16", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 16>},
-        {"fwd u8->i8 pers2 w20", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 20>},
-        {"fwd u8->i8 pers2 w8", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 8>},
-        {"fwd u8->i8 pers2 w12", launch_i8_pers_w<F | N | W512 | IP | kVarPersist2, 12>},
+        {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 two sets", launch_i8_two<F | N | W512 | IP | kVarTwoSets>},
+        {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 two sets b256", launch_i8_two<F | N | IP | kVarTwoSets>},
+        {"u8->f32 tile", launch_fwd_any<uint8_t, float, B | W512>},
+        {"u8->f32 two sets", launch_f32_two<B | W512 | kVarTwoSets>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
         {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
