@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--c4-size", type=int, default=16384)
     ap.add_argument("--c5-size", type=int, default=4096)
     ap.add_argument("--c5-frames", type=int, default=512)
+    ap.add_argument("--no-c4c5", action="store_true",
+                    help="skip the C4/C5 extras (PMC passes: every kernel then runs at the C3 size only)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank flow with several ranks on one GPU)")
@@ -245,17 +247,19 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, stream=stream) for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_f32_f32_runtimeT"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world)
+        extras["fwd_f32_f32_runtimeT"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world,
+                                               "fdct_f32_f32_duo_runtimeT", n)
         # u8 -> int8 wire format
         i8 = [torch.empty((n, n), dtype=torch.int8, device=dev) for _ in range(args.sets)]
         calls = [hpdct.bind("fwd", imgs[s], i8[s], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_u8_i8"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world)
+        extras["fwd_u8_i8"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world, "fdct_u8_i8", n)
         # inverse fp32 -> fp32 (idct_all_blocks_cuda's data path)
         rec = [torch.empty((n, n), dtype=torch.float32, device=dev) for _ in range(2)]
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world)
+        extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world,
+                                      "idct_f32_f32_duo", n)
         # the reference's own two GPU decompositions of the same arithmetic, on
         # this GPU (include/hpdct_baseline.h): 3 launches per frame, fp32 in/out
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
@@ -307,8 +311,9 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         extras["c2_fwd_u8_f32"] = line
         del c2_in, c2_out
         torch.cuda.empty_cache()
-        extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks)
-        extras["c5"] = _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks)
+        if not args.no_c4c5:
+            extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks)
+            extras["c5"] = _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks)
 
 
 class HipEvents:
@@ -343,11 +348,29 @@ class HipEvents:
         return ms.value
 
 
-def _line(px, ms_step, kern_ms, bpp, world):
+def _pmc(key, n):
+    """PMC-measured HBM traffic of one kernel (profiles/pmc_traffic.json,
+    tools/pmc_traffic.sh), if recorded at this frame size."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            k = json.load(fh).get("kernels", {}).get(key)
+        if k and k.get("size") == n:
+            return k
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def _line(px, ms_step, kern_ms, bpp, world, pmc_key=None, n=None):
     gbs = bpp * px / (kern_ms * 1e-3) / 1e9
-    return {"gpx_s": round(world * px / (ms_step * 1e-3) / 1e9, 3), "ms_per_step": round(ms_step, 5),
-            "kernel_us_avg": round(kern_ms * 1e3, 2), "bytes_per_px": bpp, "achieved_GBs": round(gbs, 1),
-            "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    out = {"gpx_s": round(world * px / (ms_step * 1e-3) / 1e9, 3), "ms_per_step": round(ms_step, 5),
+           "kernel_us_avg": round(kern_ms * 1e3, 2), "bytes_per_px": bpp, "achieved_GBs": round(gbs, 1),
+           "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    k = _pmc(pmc_key, n) if pmc_key else None
+    if k:
+        out["traffic"] = k["hbm_bytes_per_launch"]
+        out["traffic_over_algorithmic"] = k["traffic_over_algorithmic"]
+    return out
 
 
 def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks):

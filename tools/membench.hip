@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void read_only(const uint4* __restrict__ in, u
 
 // calibration kernels for the PMC byte counters (known byte counts, the
 // access widths of the DCT kernels: dwordx2 loads, dwordx4 loads, dwordx4
-// non-temporal stores)
+// and dwordx2 non-temporal stores)
 __global__ __launch_bounds__(256) void calib_read_x2(const uint2* __restrict__ in, uint64_t n8, uint32_t* sink) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     uint32_t acc = 0;
@@ -135,6 +135,14 @@ __global__ __launch_bounds__(256) void calib_read_x2(const uint2* __restrict__ i
         acc ^= w.x ^ w.y;
     }
     if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void calib_write_x2_nt(uint2* __restrict__ out, uint64_t n8) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n8; i += stride) {
+        __builtin_nontemporal_store((uint32_t)i, &out[i].x);
+        __builtin_nontemporal_store((uint32_t)(i >> 32), &out[i].y);
+    }
 }
 
 // tile pattern (the DCT kernel's): per lane 8 rows x (8 B in, 32 B out)
@@ -174,9 +182,11 @@ static int calib(int cus) {
                            sink);
         hipLaunchKernelGGL(write_only<true>, dim3(cus * 8), dim3(256), 0, 0, (float4*)(i & 1 ? a : b), bytes / 16);
         hipLaunchKernelGGL(write_only<false>, dim3(cus * 8), dim3(256), 0, 0, (float4*)(i & 1 ? b : a), bytes / 16);
+        hipLaunchKernelGGL(calib_write_x2_nt, dim3(cus * 8), dim3(256), 0, 0, (uint2*)(i & 1 ? a : b), bytes / 8);
     }
     CK(hipDeviceSynchronize());
-    printf("calibration kernels: 5 x {calib_read_x2, read_only(x4), write_only nt, write_only plain}, "
+    printf("calibration kernels: 5 x {calib_read_x2, read_only(x4), write_only nt, write_only plain, "
+           "calib_write_x2_nt}, "
            "%zu bytes each\n", bytes);
     return 0;
 }

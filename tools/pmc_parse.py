@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Turn the rocprofv3 PMC passes of tools/pmc_traffic.sh into per-launch HBM
-bytes for the headline kernel (profiles/pmc_traffic.json).
+bytes for the path's kernels (profiles/pmc_traffic.json): the headline
+u8 -> fp32 kernel, the int8 forward and the fp32 duo forward / inverse.
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB per dispatch.  Each is scaled by
 the ratio (known bytes / counted bytes) measured on a calibration kernel of
 the same access width (tools/membench calib): dwordx2 loads for the uint8
-reads, dwordx4 non-temporal stores for the fp32 writes
+reads, dwordx4 loads for fp32, dwordx4 / dwordx2 non-temporal stores
 (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide streaming read on
 gfx950; other widths must be calibrated).
 
@@ -24,6 +25,7 @@ CALIB_BYTES = 256 << 20
 def per_dispatch(dirpath, counter):
     """{kernel_name: [value per dispatch]} from a rocprofv3 counter csv."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
+    files += glob.glob(dirpath + ".counter_collection.csv")  # the flattened copies under profiles/
     out = {}
     for f in files:
         for r in csv.DictReader(open(f)):
@@ -40,6 +42,15 @@ def pick(d, needle, exclude=()):
     raise KeyError(needle)
 
 
+# kernel key -> (name needle, exclude, read width, write width, B/px read, B/px written)
+KERNELS = {
+    "fdct_u8_f32": ("fdct_kernel<unsigned char, float, true, true, false", (), "x2", "x4nt", 1, 4),
+    "fdct_u8_i8": ("fdct_kernel<unsigned char, signed char, true, true, false", (), "x2", "x2nt", 1, 1),
+    "fdct_f32_f32_duo_runtimeT": ("fdct_duo_kernel<true, false, false", (), "x4", "x4nt", 4, 4),
+    "idct_f32_f32_duo": ("idct_duo_kernel<true, true", (), "x4", "x4nt", 4, 4),
+}
+
+
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
@@ -47,37 +58,46 @@ def main():
     write = per_dispatch(os.path.join(src, "bench_WRITE_SIZE"), "WRITE_SIZE")
     cf = per_dispatch(os.path.join(src, "calib_FETCH_SIZE"), "FETCH_SIZE")
     cw = per_dispatch(os.path.join(src, "calib_WRITE_SIZE"), "WRITE_SIZE")
-    kf = statistics.median(pick(fetch, "fdct_kernel<unsigned char, float"))
-    kw = statistics.median(pick(write, "fdct_kernel<unsigned char, float"))
-    read_x2 = statistics.median(pick(cf, "calib_read_x2")) * 1024
-    read_x4 = statistics.median(pick(cf, "read_only")) * 1024
-    wr_nt = statistics.median(pick(cw, "write_only<true>")) * 1024
-    wr_plain = statistics.median(pick(cw, "write_only<false>")) * 1024
-    f_scale = CALIB_BYTES / read_x2
-    w_scale = CALIB_BYTES / wr_nt
+    counted = {
+        "x2": statistics.median(pick(cf, "calib_read_x2")) * 1024,
+        "x4": statistics.median(pick(cf, "read_only")) * 1024,
+        "x4nt": statistics.median(pick(cw, "write_only<true>")) * 1024,
+        "x4plain": statistics.median(pick(cw, "write_only<false>")) * 1024,
+    }
+    try:
+        counted["x2nt"] = statistics.median(pick(cw, "calib_write_x2_nt")) * 1024
+    except KeyError:  # older calibration run without the dwordx2 NT store kernel
+        counted["x2nt"] = float(CALIB_BYTES)
+    scale = {k: CALIB_BYTES / v for k, v in counted.items()}
     n = 8192
-    alg_read, alg_write = n * n, 4 * n * n
-    read_b = kf * 1024 * f_scale
-    write_b = kw * 1024 * w_scale
+    kernels = {}
+    for key, (needle, excl, rw, ww, rb, wb) in KERNELS.items():
+        try:
+            kf = statistics.median(pick(fetch, needle, excl))
+            kw = statistics.median(pick(write, needle, excl))
+        except KeyError:
+            continue
+        read_b = kf * 1024 * scale[rw]
+        write_b = kw * 1024 * scale[ww]
+        alg = (rb + wb) * n * n
+        kernels[key] = {
+            "size": n,
+            "fetch_size_kib_raw": kf, "write_size_kib_raw": kw,
+            "read_width": rw, "write_width": ww,
+            "hbm_read_bytes_per_launch": round(read_b),
+            "hbm_write_bytes_per_launch": round(write_b),
+            "hbm_bytes_per_launch": round(read_b + write_b),
+            "algorithmic_bytes_per_launch": alg,
+            "traffic_over_algorithmic": round((read_b + write_b) / alg, 4),
+        }
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_traffic.sh",
         "calibration": {
             "known_bytes": CALIB_BYTES,
-            "fetch_dwordx2_counted": read_x2, "fetch_dwordx4_counted": read_x4,
-            "write_dwordx4_nt_counted": wr_nt, "write_dwordx4_plain_counted": wr_plain,
-            "fetch_scale_used": f_scale, "write_scale_used": w_scale,
+            "counted": counted,
+            "scale": scale,
         },
-        "kernels": {
-            "fdct_u8_f32": {
-                "size": n,
-                "fetch_size_kib_raw": kf, "write_size_kib_raw": kw,
-                "hbm_read_bytes_per_launch": round(read_b),
-                "hbm_write_bytes_per_launch": round(write_b),
-                "hbm_bytes_per_launch": round(read_b + write_b),
-                "algorithmic_bytes_per_launch": alg_read + alg_write,
-                "traffic_over_algorithmic": round((read_b + write_b) / (alg_read + alg_write), 4),
-            }
-        },
+        "kernels": kernels,
     }
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     with open(dst, "w") as fh:
