@@ -52,6 +52,8 @@ enum : unsigned {
                                 // compute of set n overlaps the loads of set n+1
     kVarTwoSets = 1u << 23,     // each wave takes two consecutive sets, all 16 row loads issued up front:
                                 // the first set's compute overlaps the second set's loads
+    kVarStSc1 = 1u << 24,       // fp32 re-staged stores as global_store_dwordx4 ... sc1 (with kVarNT: sc1 nt)
+    kVarStSc0Sc1 = 1u << 25,    // ... sc0 sc1 (with kVarNT: sc0 sc1 nt)
     kVarPacked = 1u << 19,      // uint8 input, built-in T, quantised: packed-fp32 transform and quotient
                                 // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, fdct_tile_pk)
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
@@ -333,7 +335,25 @@ __device__ __forceinline__ void store_row(TOut* __restrict__ row, const float (&
 // Optional slot swizzle sw(k) = k ^ ((k >> 3) & 1) (an involution that keeps
 // [0,64) and [64,128)): the deposits of 8 consecutive lanes then hit 8
 // distinct 16-B bank groups; the pick-up of slot j stores to position sw(j).
-template <bool kNT, bool kSwz>
+// 16-byte store with an explicit cache policy (kPol: 0 = st<kNT>, 1 = sc1,
+// 2 = sc0 sc1; kNT adds nt) through a raw buffer store, whose aux operand
+// carries the gfx940+ cache-policy bits (sc0 = 1, nt = 2, sc1 = 16); inline
+// asm is not an option: the compiler would not track the store's read of its
+// data registers.  `base` is wave-uniform, `off` the lane's byte offset.
+template <bool kNT, int kPol>
+__device__ __forceinline__ void st_pol(float* base, uint32_t off, const float4& v) {
+    if constexpr (kPol == 0) {
+        st<kNT>(reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + off), v);
+    } else {
+        constexpr int kAux = (kPol == 1 ? 16 : 17) | (kNT ? 2 : 0);
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+        const v4i w = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, rsrc, off, 0, kAux);
+    }
+}
+
+template <bool kNT, bool kSwz, int kPol = 0>
 __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* __restrict__ seg, uint32_t lane,
                                               const float (&c)[8]) {
     auto sw = [](uint32_t k) { return kSwz ? (k ^ ((k >> 3) & 1u)) : k; };
@@ -341,8 +361,8 @@ __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* 
     slot[sw(2 * lane + 1)] = make_float4(c[4], c[5], c[6], c[7]);
     const float4 a = slot[lane];
     const float4 b = slot[64 + lane];
-    st<kNT>(reinterpret_cast<float4*>(seg) + sw(lane), a);
-    st<kNT>(reinterpret_cast<float4*>(seg) + 64 + sw(lane), b);
+    st_pol<kNT, kPol>(seg, 16u * sw(lane), a);
+    st_pol<kNT, kPol>(seg, 16u * (64u + sw(lane)), b);
 }
 
 // Per-wave walk over 64-tile sets: one set per wave (plain), or a grid-stride
@@ -471,8 +491,9 @@ struct RowSink {
                                                const float (&c)[8]) const {
         if constexpr (kLds) {
             if (seg_ok) {
-                store_row_lds<kNT, (kVar & kVarLdsSwz) != 0>(slots + (v & 1) * 128, plane + seg + v * width,
-                                                             threadIdx.x & 63u, c);
+                constexpr int kPol = (kVar & kVarStSc1) ? 1 : (kVar & kVarStSc0Sc1) ? 2 : 0;
+                store_row_lds<kNT, (kVar & kVarLdsSwz) != 0, kPol>(slots + (v & 1) * 128,
+                                                                   plane + seg + v * width, threadIdx.x & 63u, c);
                 return;
             }
         }

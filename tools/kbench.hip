@@ -366,6 +366,11 @@ int main(int argc, char** argv) {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
         {"u8->f32 tile (product)", launch_var<B | W512>},
         {"u8->f32 tile packed", launch_var<B | W512 | PK>},
+        {"u8->f32 tile st sc1 nt", launch_var<B | W512 | kVarStSc1>},
+        {"u8->f32 tile st sc1", launch_var<(B & ~N) | W512 | kVarStSc1>},
+        {"u8->f32 tile st sc0sc1 nt", launch_var<B | W512 | kVarStSc0Sc1>},
+        {"u8->f32 tile st sc0sc1", launch_var<(B & ~N) | W512 | kVarStSc0Sc1>},
+        {"u8->f32 tile plain st", launch_var<(B & ~N) | W512>},
         {"u8->f32 octet", launch_fwd_oct<uint8_t, float, F | N | OR>},
     };
     // pairs (2k, 2k+1), checked bit-exact against each other
