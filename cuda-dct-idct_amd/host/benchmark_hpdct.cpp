@@ -4,7 +4,10 @@
 // rand()%256 stored as float, :44-51), same Q/T tables, same call sequence
 // (H2D -> dct_all_blocks_cuda -> D2H -> idct_all_blocks_cuda -> D2H) and the
 // same stdout lines "DCT (W,H): x ms" / "IDCT (W,H): x ms", printed by the
-// library's compat entry points.
+// library's compat entry points.  An optional second argument repeats the
+// whole sequence (image re-uploaded each time, since the forward leaves X-128
+// in it) to average warm calls; the first call of a process includes loading
+// the kernels' code object.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,11 +24,12 @@
     }
 
 int main(int argc, char* argv[]) {
-    if (argc != 2) {
-        printf("Use: %s <width/height>\n", argv[0]);
+    if (argc != 2 && argc != 3) {
+        printf("Use: %s <width/height> [runs]\n", argv[0]);
         return 1;
     }
     const size_t n = strtoul(argv[1], NULL, 10);
+    const long runs = argc == 3 ? strtol(argv[2], NULL, 10) : 1;
     const size_t width = n, height = n;
     const size_t px = width * height;
 
@@ -42,15 +46,16 @@ int main(int argc, char* argv[]) {
     CHECK_HIP(hipMalloc(&d_A, px * sizeof(float)));
     CHECK_HIP(hipMalloc(&d_B, 64 * sizeof(float)));
     CHECK_HIP(hipMalloc(&d_C, px * sizeof(float)));
-    CHECK_HIP(hipMemcpy(d_A, image, px * sizeof(float), hipMemcpyHostToDevice));
     CHECK_HIP(hipMemcpy(d_B, transform, 64 * sizeof(float), hipMemcpyHostToDevice));
-
-    dct_all_blocks_cuda(d_A, (int)height, (int)width, d_B, d_C);
-    CHECK_HIP(hipMemcpy(result, d_C, px * sizeof(float), hipMemcpyDeviceToHost));
-
     CHECK_HIP(hipMalloc(&d_E, px * sizeof(float)));
-    idct_all_blocks_cuda(d_C, (int)height, (int)width, d_B, d_E);
-    CHECK_HIP(hipMemcpy(result, d_E, px * sizeof(float), hipMemcpyDeviceToHost));
+
+    for (long r = 0; r < (runs > 0 ? runs : 1); ++r) {
+        CHECK_HIP(hipMemcpy(d_A, image, px * sizeof(float), hipMemcpyHostToDevice));
+        dct_all_blocks_cuda(d_A, (int)height, (int)width, d_B, d_C);
+        CHECK_HIP(hipMemcpy(result, d_C, px * sizeof(float), hipMemcpyDeviceToHost));
+        idct_all_blocks_cuda(d_C, (int)height, (int)width, d_B, d_E);
+        CHECK_HIP(hipMemcpy(result, d_E, px * sizeof(float), hipMemcpyDeviceToHost));
+    }
 
     CHECK_HIP(hipFree(d_A));
     CHECK_HIP(hipFree(d_B));

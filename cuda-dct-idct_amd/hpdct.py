@@ -266,8 +266,8 @@ def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, 
     return out
 
 
-def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift=True, stream=None,
-         height=None, width=None):
+def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift=True, writeback_shift=False,
+         stream=None, height=None, width=None):
     """Pre-resolve every argument of one forward ("fwd") or inverse ("inv")
     launch and return a zero-argument callable: the per-call host cost is one
     ctypes call (used by bench.py's timed loop)."""
@@ -276,7 +276,8 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
     h, w = _hw(src, height, width)
     lib = load_library()
     fn = {"fwd": lib.hpdct_forward, "inv": lib.hpdct_inverse}[direction]
-    flags = (0 if quantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT)
+    flags = (0 if quantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT) | \
+        (FLAG_WRITEBACK_SHIFT if writeback_shift else 0)
     args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(dst.data_ptr()), _dtype_code(dst),
             h, w, None if transform is None else ctypes.c_void_p(transform.data_ptr()), flags, _stream_ptr(stream))
 
