@@ -30,6 +30,15 @@ def test_benchmark_cli():
     assert p.returncode == 1 and "Use:" in p.stdout
 
 
+def test_benchmark_cli_repeated_runs():
+    """Optional run count (tools/size_sweep.py): the reference's call sequence
+    and lines repeated, one DCT and one IDCT line per run."""
+    p = run([os.path.join(BIN, "benchmark_hpdct"), "64", "3"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert len(re.findall(r"^DCT \(64,64\): [0-9.]+ ms$", p.stdout, re.M)) == 3
+    assert len(re.findall(r"^IDCT \(64,64\): [0-9.]+ ms$", p.stdout, re.M)) == 3
+
+
 def _write_pgm(path, img):
     with open(path, "wb") as fh:
         fh.write(b"P5\n%d %d\n255\n" % (img.shape[1], img.shape[0]))
