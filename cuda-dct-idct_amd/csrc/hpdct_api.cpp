@@ -58,12 +58,6 @@ int mapping_from_env() {
     return HPDCT_MAPPING_AUTO;
 }
 
-std::mutex g_q_mutex;
-Mat64 g_q = [] {
-    Mat64 m;
-    memcpy(m.v, kDefaultQ, sizeof(m.v));
-    return m;
-}();
 
 thread_local std::string g_last_error;
 
@@ -75,11 +69,6 @@ hpdct_status fail(hpdct_status st, const std::string& msg) {
 hpdct_status device_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return HPDCT_SUCCESS;
     return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-Mat64 current_q() {
-    std::lock_guard<std::mutex> lk(g_q_mutex);
-    return g_q;
 }
 
 // max |q| the forward quantiser can produce for uint8 input with the built-in T:
@@ -126,6 +115,29 @@ QParams make_qparams(const Mat64& q) {
     p.q = q;
     for (int i = 0; i < 64; ++i) p.r.v[i] = 1.0f / q.v[i];  // RN(1/Q), as the verification tools compute it
     return p;
+}
+
+// The library-owned quantiser: the table, its reciprocals and the two
+// properties the launches need, computed once per hpdct_set_quant_table
+// (not per call) and copied out under the mutex.
+struct QState {
+    QParams qp;
+    bool fastdiv_ok;  // integers in 1..255: the verified 3-op quotient is exact
+    bool int8_ok;     // |q| <= 127 for uint8 input with the built-in T
+};
+
+QState make_qstate(const Mat64& q) { return QState{make_qparams(q), fastdiv_table(q), int8_safe(q)}; }
+
+std::mutex g_q_mutex;
+QState g_qs = [] {
+    Mat64 m;
+    memcpy(m.v, kDefaultQ, sizeof(m.v));
+    return make_qstate(m);
+}();
+
+QState current_qstate() {
+    std::lock_guard<std::mutex> lk(g_q_mutex);
+    return g_qs;
 }
 
 bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
@@ -178,15 +190,16 @@ hpdct_status hpdct_set_quant_table(const float* q64) {
                 return fail(HPDCT_ERROR_INVALID_VALUE, "quant table entries must be finite and non-zero");
         memcpy(m.v, q64, sizeof(m.v));
     }
+    const QState qs = make_qstate(m);
     std::lock_guard<std::mutex> lk(g_q_mutex);
-    g_q = m;
+    g_qs = qs;
     return HPDCT_SUCCESS;
 }
 
 hpdct_status hpdct_get_quant_table(float* q64) {
     if (!q64) return fail(HPDCT_ERROR_INVALID_VALUE, "null output pointer");
-    const Mat64 m = current_q();
-    memcpy(q64, m.v, sizeof(m.v));
+    const QState qs = current_qstate();
+    memcpy(q64, qs.qp.q.v, sizeof(qs.qp.q.v));
     return HPDCT_SUCCESS;
 }
 
@@ -222,12 +235,12 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     const size_t out_bytes = static_cast<size_t>(height) * width * elem_size(out_type);
     if (ib < ob + out_bytes && ob < ib + in_bytes)
         return fail(HPDCT_ERROR_INVALID_VALUE, "image and coefficient buffers overlap");
-    const Mat64 q = current_q();
-    if (out_type == HPDCT_I8 && !int8_safe(q))
+    const QState qs = current_qstate();
+    if (out_type == HPDCT_I8 && !qs.int8_ok)
         return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
-    const QParams qp = make_qparams(q);
+    const QParams& qp = qs.qp;
     // |C| <= 8*255 for uint8 input with the built-in T, well inside the verified |C| <= 4096
-    const bool fastdiv = quant && in_type == HPDCT_U8 && d_transform == nullptr && fastdiv_table(q);
+    const bool fastdiv = quant && in_type == HPDCT_U8 && d_transform == nullptr && qs.fastdiv_ok;
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool bt = d_transform == nullptr;
@@ -290,7 +303,7 @@ hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_imag
         return fail(HPDCT_ERROR_UNSUPPORTED, "ROW_FIRST / WRITEBACK_DEQUANT are fp32 -> fp32 (cublasDCTv2) options");
     if (wb && !deq) return fail(HPDCT_ERROR_UNSUPPORTED, "HPDCT_FLAG_WRITEBACK_DEQUANT needs dequantisation");
     float* dq_out = wb ? static_cast<float*>(const_cast<void*>(d_coef)) : nullptr;
-    const Mat64 q = current_q();
+    const Mat64 q = current_qstate().qp.q;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool bt = d_transform == nullptr;
     hipError_t e = hipSuccess;
