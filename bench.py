@@ -290,13 +290,26 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         sx = float((x * x).sum())
         se = float(((x - r.double()) ** 2).sum())
         se8 = float(((x - r8.double()) ** 2).sum())
+        # the same round trip in ONE pass (hpdct_roundtrip_u8): fp32 coefficients
+        # + uint8 reconstruction + the PEEN/MSE sums, 6 B/px of HBM
+        sums_buf = torch.zeros(3, dtype=torch.int64, device=dev)
+        one = [hpdct.bind_roundtrip(imgs[s], outs[s], rt_px[s % 2], sums_buf, stream=stream)
+               for s in range(args.sets)]
+        rms1, k1, _ = timed_loop(one, steps, 4)
+        one[0]()
+        qd = hpdct.quality_from_sums(hpdct.sums_from_buffer(sums_buf), px)
+        one_ms = rms1 / steps
         extras["c3_roundtrip"] = {
             "mse_f32": se / px, "peen_f32_pct": 100.0 * (se / sx) ** 0.5,
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
-            "ms_per_frame_fwd_inv_u8": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
-            "bytes_per_px": 10,
+            "two_kernels": {"ms_per_frame": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
+                            "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
+            "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world),
+                             quality_from_device_sums=qd,
+                             note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums, one "
+                                  "kernel; bit-identical to the two kernels"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
-        del f32_in, i8, rec, r8, x, rt_px
+        del f32_in, i8, rec, r8, x, rt_px, sums_buf
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024

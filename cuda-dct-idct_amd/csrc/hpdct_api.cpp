@@ -337,6 +337,43 @@ hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_imag
     return device_status(e, "inverse kernel launch");
 }
 
+hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
+                                hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream) {
+    static_assert(sizeof(hpdct_roundtrip_sums) == sizeof(hpdct::RtSums), "hpdct_roundtrip_sums layout");
+    TileGrid g;
+    if (hpdct_status st = make_grid(height, width, g)) return st;
+    if (!d_image || !d_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "null image or coefficient pointer");
+    if (d_recon && recon_type != HPDCT_U8 && recon_type != HPDCT_F32)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "reconstruction must be HPDCT_U8 or HPDCT_F32");
+    if (!aligned(d_image, 8) || !aligned(d_coef, 16) || (d_recon && !aligned(d_recon, row_align(recon_type))) ||
+        (d_sums && !aligned(d_sums, 8)))
+        return fail(HPDCT_ERROR_INVALID_VALUE,
+                    "device pointers must be 16-byte (fp32) / 8-byte (8-bit planes, sums) aligned");
+    const size_t px = static_cast<size_t>(height) * width;
+    struct Span {
+        const char* p;
+        size_t n;
+    };
+    const Span spans[4] = {{static_cast<const char*>(static_cast<const void*>(d_image)), px},
+                           {reinterpret_cast<const char*>(d_coef), px * 4},
+                           {static_cast<const char*>(d_recon), d_recon ? px * elem_size(recon_type) : 0},
+                           {reinterpret_cast<const char*>(d_sums), d_sums ? sizeof(hpdct_roundtrip_sums) : 0}};
+    for (int a = 0; a < 4; ++a)
+        for (int b = a + 1; b < 4; ++b)
+            if (spans[a].n && spans[b].n && spans[a].p < spans[b].p + spans[b].n &&
+                spans[b].p < spans[a].p + spans[a].n)
+                return fail(HPDCT_ERROR_INVALID_VALUE, "image, coefficient, reconstruction and sums buffers overlap");
+    const QState qs = current_qstate();
+    // packed int8 rows + the verified quotient when both properties hold, else
+    // IEEE division with the rows kept in fp32 (any finite non-zero table)
+    const bool fast = qs.fastdiv_ok && qs.int8_ok;
+    const int kind = !d_recon ? hpdct::kRtReconNone : recon_type == HPDCT_U8 ? hpdct::kRtReconU8 : hpdct::kRtReconF32;
+    return device_status(hpdct::launch_roundtrip(d_image, d_coef, d_recon, kind,
+                                                 reinterpret_cast<hpdct::RtSums*>(d_sums), g, qs.qp, fast,
+                                                 static_cast<hipStream_t>(stream)),
+                         "round-trip kernel launch");
+}
+
 hpdct_status hpdct_forward_u8_f32(const uint8_t* d_image, float* d_coef, int64_t height, int64_t width,
                                   void* stream) {
     return hpdct_forward(d_image, HPDCT_U8, d_coef, HPDCT_F32, height, width, nullptr, 0u, stream);

@@ -153,9 +153,26 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
     duo_store<kVar>(out, g, run, run_base, p.base, p.valid, slot_all, t, h, o);
 }
 
-// Inverse, duo mapping, fp32 coefficients -> fp32 pixels.  Arguments as idct_kernel.
-template <bool kDequant, bool kBuiltinT, unsigned kVar>
-__global__ __launch_bounds__(kBlock<kVar>) void idct_duo_kernel(const float* __restrict__ coef, float* __restrict__ out,
+// uint8 pixels (clamp + truncate, utils.cu:21): the lane's rows 4h..4h+3, one
+// 8-byte store each; per instruction the wave writes row k and row 4+k of its
+// 32 tiles, two 256-B runs.
+template <unsigned kVar>
+__device__ __forceinline__ void duo_store(uint8_t* __restrict__ plane, const TileGrid& g, bool, uint64_t,
+                                          uint64_t base, bool valid, float*, uint32_t, uint32_t h,
+                                          const float (&o)[4][8]) {
+    constexpr bool kNT = (kVar & kVarNT) != 0;
+    if (valid) {
+        unroll<4>([&](auto k) {
+            st<kNT>(reinterpret_cast<uint2*>(plane + base + (4u * h + k) * g.width),
+                    make_uint2(pack_u8x4(o[k][0], o[k][1], o[k][2], o[k][3]),
+                               pack_u8x4(o[k][4], o[k][5], o[k][6], o[k][7])));
+        });
+    }
+}
+
+// Inverse, duo mapping, fp32 coefficients -> fp32 or uint8 pixels.  Arguments as idct_kernel.
+template <bool kDequant, bool kBuiltinT, unsigned kVar, typename TOut = float>
+__global__ __launch_bounds__(kBlock<kVar>) void idct_duo_kernel(const float* __restrict__ coef, TOut* __restrict__ out,
                                                                 float* __restrict__ dq_out, TileGrid g,
                                                                 const float* __restrict__ t_dev, Mat64 q,
                                                                 float shift) {

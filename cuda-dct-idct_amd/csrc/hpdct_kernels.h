@@ -43,6 +43,21 @@ template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
 hipError_t launch_idct(const TIn* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
                        const Mat64& q, float shift, bool row_first, hipStream_t s);
 
+// Round trip (hpdct_roundtrip.hpp): uint8 frame -> fp32 quantised
+// coefficients + optional reconstruction + optional quality sums, built-in T.
+// Device accumulators, the layout of hpdct_roundtrip_sums (include/hpdct.h).
+struct RtSums {
+    unsigned long long sse_f32_fx;  // sum (x - (R+128))^2 * 2^16, per-tile fp32 sums rounded
+    unsigned long long sse_u8;      // sum (x - u8(R+128))^2, exact
+    unsigned long long sum_x2;      // sum x^2, exact
+};
+enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
+// fast: integer table in 1..255 with int8-range quotients (verified quotient,
+// packed int8 rows); sums may be nullptr (no statistics), recon nullptr with
+// kRtReconNone.  Zeroes *sums on the stream before the kernel.
+hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
+                            const TileGrid& g, const QParams& qp, bool fast, hipStream_t s);
+
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.

@@ -59,6 +59,10 @@ enum : unsigned {
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
                                 // all finite -> the zero terms of T are skipped (exact: a chain from +0
                                 // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
+    kVarPrio = 1u << 26,        // s_setprio 3 while the wave computes its addresses and issues its loads
+    // diagnostics only (tools/kbench): split the kernel's time into its phases
+    kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
+    kVarNoStore = 1u << 28,     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
@@ -82,12 +86,28 @@ __device__ __forceinline__ uint32_t pack_i8x4(float a, float b, float c, float d
     return ia | (ib << 8) | (ic << 16) | (id << 24);
 }
 
-// convertToUnsignedChar (utils.cu:21): (unsigned char)fminf(fmaxf(x, 0), 255)
-__device__ __forceinline__ uint32_t to_u8(float x) {
-    return static_cast<uint32_t>(__builtin_fminf(__builtin_fmaxf(x, 0.0f), 255.0f));
+// convertToUnsignedChar (utils.cu:21): (unsigned char)fminf(fmaxf(x, 0), 255),
+// two operations per pixel: v_cvt_u32_f32 truncates and saturates (NaN and
+// negatives -> 0, +inf -> 0xffffffff), then min(., 255) is written straight
+// into byte k of the packed word (SDWA dst_sel).  Same value for every fp32
+// input, NaN and infinities included (tests/test_gpu_parity.py extremes).
+__device__ __forceinline__ uint32_t cvt_u32_sat(float x) {
+    uint32_t t;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(t) : "v"(x));
+    return t;
 }
 __device__ __forceinline__ uint32_t pack_u8x4(float a, float b, float c, float d) {
-    return to_u8(a) | (to_u8(b) << 8) | (to_u8(c) << 16) | (to_u8(d) << 24);
+    const uint32_t k255 = 255u;
+    uint32_t w;
+    asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+        : "=v"(w) : "v"(cvt_u32_sat(a)), "v"(k255));
+    asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(w) : "v"(cvt_u32_sat(b)), "v"(k255));
+    asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(w) : "v"(cvt_u32_sat(c)), "v"(k255));
+    asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(w) : "v"(cvt_u32_sat(d)), "v"(k255));
+    return w;
 }
 
 // roundf (round half away from zero) in three operations:
@@ -432,12 +452,17 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         }
     } else if constexpr (!kPersist) {
         if (wave >= nsets) return;
+        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(3);
         const TilePos p = tile_pos(g, wave * 64u + lane);
         uint64_t seg;
         const bool ok = seg_info(wave, p, seg);
         if (!p.valid) return;
         RawTile<TIn> raw;
-        if constexpr ((kVar & kVarLdsLoad) != 0 && std::is_same_v<TIn, float>) {
+        if constexpr ((kVar & kVarNoLoad) != 0 && sizeof(TIn) == 1) {
+            unroll<8>([&](auto i) {
+                raw.r[i] = make_uint2((lane * 0x01010101u) ^ (i * 0x10325476u), (lane * 0x03050709u) + i);
+            });
+        } else if constexpr ((kVar & kVarLdsLoad) != 0 && std::is_same_v<TIn, float>) {
             if (ok) {
                 raw.load_staged(src + seg, g.width, lane, slots);
             } else {
@@ -448,6 +473,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         } else {
             raw.load(src + p.base, g.width);
         }
+        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(0);
         body(raw, p, ok, seg);
     } else {
         const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
@@ -605,6 +631,9 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
             if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
                 unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
                 const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
+                if constexpr ((kVar & kVarNoStore) != 0) {
+                    if (g.ntiles != 0xffffffffu) return;
+                }
                 st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
                 return;
             }

@@ -100,11 +100,11 @@ hipError_t fdct_duo_go(const float* img, float* out, float* shifted, const TileG
     return hipGetLastError();
 }
 
-template <unsigned kV, bool kDequant, bool kBuiltinT>
-hipError_t idct_duo_go(const float* coef, float* out, float* dq_out, const TileGrid& g, const float* t_dev,
+template <unsigned kV, bool kDequant, bool kBuiltinT, typename TOut>
+hipError_t idct_duo_go(const float* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
                        const Mat64& q, float shift, hipStream_t s) {
-    hipLaunchKernelGGL((idct_duo_kernel<kDequant, kBuiltinT, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>), 0, s,
-                       coef, out, dq_out, g, t_dev, q, shift);
+    hipLaunchKernelGGL((idct_duo_kernel<kDequant, kBuiltinT, kV, TOut>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>), 0,
+                       s, coef, out, dq_out, g, t_dev, q, shift);
     return hipGetLastError();
 }
 
@@ -199,15 +199,20 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
         }
     }
     (void)row_first;
-    const Mapping map = pick_mapping(g, kF32);
-    if constexpr (kF32) {
+    // fp32 coefficients -> fp32 or uint8 pixels: the duo kernel's 1 KiB row loads
+    // (8192^2 -> uint8: 61.8 -> 56.7 us, profiles/r01/mappings/kbench2_inv_i8.log)
+    constexpr bool kDuoIn = std::is_same_v<TIn, float> && (kF32 || std::is_same_v<TOut, uint8_t>);
+    const Mapping map = pick_mapping(g, kDuoIn);
+    if constexpr (kDuoIn) {
+        // uint8 output: 512-thread workgroups (56.7 vs 57.6 us with 256)
+        constexpr unsigned kDV = std::is_same_v<TOut, uint8_t> ? (kDuoVar | (2u << 12)) : kDuoVar;
         if (map == Mapping::kDuo) {
             if constexpr (kDequant) {
                 if (dq_out)
-                    return idct_duo_go<kDuoVar | kVarWbDequant, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q,
-                                                                                   shift, s);
+                    return idct_duo_go<kDV | kVarWbDequant, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q,
+                                                                               shift, s);
             }
-            return idct_duo_go<kDuoVar, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
+            return idct_duo_go<kDV, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
         }
     }
     if (map == Mapping::kOctet) {

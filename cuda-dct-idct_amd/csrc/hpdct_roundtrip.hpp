@@ -1,0 +1,218 @@
+// hpdct_roundtrip.hpp -- the C3 round trip in one HBM pass: uint8 frame ->
+// fp32 quantised coefficients + reconstruction (+ the PEEN/MSE sums), for
+// CDNA4 / gfx950.
+//
+// The reference runs a round trip as dct_all_blocks_cuda then
+// idct_all_blocks_cuda (main_newAppr.cu:99,120; benchmark_newAppr.cu:93,105),
+// six launches and three fp32 planes through HBM each way; the quality check
+// (README.md:62-69) happens on the host.  Here one lane keeps its 8x8 tile in
+// VGPRs from the pixel load to the reconstructed pixel: the forward emits each
+// quantised row (stored as the fp32 coefficient row) and keeps it as 8 packed
+// int8 values; the inverse starts from those registers.  Arithmetic is the
+// forward kernel's followed by the inverse kernel's, so coefficients and
+// reconstruction are bit-identical to hpdct_forward + hpdct_inverse.
+//
+// HBM per pixel: 1 B read + 4 B coefficients (+ 1 B uint8 or 4 B fp32
+// reconstruction) written, against 1 + 4 + 4 + 1 for the two kernels.
+//
+// Quality sums (kStats), per frame, as hpdct_quality.py defines them:
+//   sum_x2  = sum x^2                       exact: v_dot4_u32_u8 on the packed
+//   sse_u8  = sum (x - u8(R+128))^2        pixel bytes (x.x, x.r8, r8.r8), uint64
+//   sse_f32 = sum (x - (R+128))^2          per tile an fp32 fma chain over the 64
+//             pixels, rounded to a multiple of 2^-16 and added as uint64: the
+//             result does not depend on the order tiles finish in.
+// Workgroup partials are added with one 64-bit atomic per field per workgroup.
+#pragma once
+
+#include "hpdct_kernels_impl.hpp"
+
+namespace hpdct {
+
+constexpr float kRtFixScale = 65536.0f;  // sse_f32 fixed point: 2^-16
+
+namespace {
+
+// unpack int8 byte k of w into an exact float (sign-extending byte convert)
+__device__ __forceinline__ float i8_byte_f32(uint32_t w, int k) {
+    return static_cast<float>(static_cast<int8_t>((w >> (8 * k)) & 0xffu));
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    unroll<6>([&](auto s) { v += __shfl_xor(v, 1 << s, 64); });
+    return v;
+}
+
+}  // namespace
+
+// kFast: integer table in 1..255 whose quotients fit int8 (library QState
+// fastdiv_ok && int8_ok): the verified 3-op quotient and the quantised rows
+// kept as packed int8 (16 VGPRs).  Otherwise IEEE division and the rows kept
+// as fp32 (64 VGPRs).
+// 512-thread workgroups, at least 4 waves per SIMD (<= 128 VGPRs: two
+// workgroups per CU); 2 with an fp32 reconstruction (its row re-staging needs
+// more registers than 128 without spilling).
+// kRaw: where the sums find the pixels again at the inverse's output rows:
+//   0  the loaded tile kept in VGPRs through both transforms (16 VGPRs)
+//   1  re-read from global memory when the inverse starts (the wave read those
+//      4 KiB microseconds earlier: served by L2 / Infinity Cache)
+//   2  stashed in LDS after the load (4 KiB per wave): the product
+// (8192^2, u8 reconstruction + sums: 89.1 / 82.7 / 72.5 us; no sums 65 us;
+// profiles/r01/mappings/kbench2_rt.log)
+template <int kRecon>
+constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
+template <int kRecon, bool kStats, bool kFast, int kRaw = 2>
+__global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
+                                                                          float* __restrict__ coef,
+                                                                          void* __restrict__ recon,
+                                                                          RtSums* __restrict__ sums, TileGrid g,
+                                                                          QParams qp) {
+    constexpr unsigned kVar = (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u);
+    const TSource<true, true> T(nullptr);  // built-in T; u8 pixels and int8-range q are finite
+    float4* const slots = wave_slots<kVar>();
+    const RowSink<kVar, float> coef_sink{coef, g.width, slots};
+    const RowSink<kVar, float> rf32_sink{static_cast<float*>(recon), g.width, slots};
+    float acc_f = 0.0f;                          // this lane's tile: sum (x - (R+128))^2
+    uint32_t acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;  // sum x^2, x.r8, r8^2 (<= 64 * 255^2)
+
+    uint2* stash = nullptr;  // kRaw == 2: this wave's [row][lane] pixel words
+    if constexpr (kStats && kRaw == 2) {
+        __shared__ uint2 raw_lds[512 / 64][8 * 64];
+        stash = raw_lds[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, bool ok, uint64_t seg) {
+        if constexpr (kStats && kRaw == 2) unroll<8>([&](auto i) { stash[i * 64u + lane] = raw.r[i]; });
+        float x[8][8];
+        raw.to_float_minus128(x);  // sub_matrix_scalar (utils_kernels.cu:16), exact: (int8)(b ^ 0x80)
+        // ---- forward: T.(X-128).T^T, round(C/Q), fp32 coefficient rows out
+        uint2 q8[8];
+        float qf[kFast ? 1 : 8][8];
+        fdct_tile(T, x, [&](auto v, float (&c)[8]) {
+            unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+            coef_sink(v, p, ok, seg, c);
+            if constexpr (kFast) {
+                // c holds integers in [-127, 127]: the truncating convert is exact
+                uint32_t w0 = 0u, w1 = 0u;
+                cvt_into_byte<0>(w0, c[0]), cvt_into_byte<1>(w0, c[1]), cvt_into_byte<2>(w0, c[2]),
+                    cvt_into_byte<3>(w0, c[3]);
+                cvt_into_byte<0>(w1, c[4]), cvt_into_byte<1>(w1, c[5]), cvt_into_byte<2>(w1, c[6]),
+                    cvt_into_byte<3>(w1, c[7]);
+                q8[v] = make_uint2(w0, w1);
+            } else {
+                unroll<8>([&](auto u) { qf[v][u] = c[u]; });
+            }
+        });
+        // ---- inverse: D = q*Q (multiply_matrices, utils_kernels.cu:55),
+        // T^T.D.T + 128 (main_newAppr.cu:220-250, utils_kernels.cu:29)
+        uint2 again[kStats && kRaw == 1 ? 8 : 1];
+        if constexpr (kStats && kRaw == 1) {
+            unroll<8>([&](auto i) { again[i] = *reinterpret_cast<const uint2*>(img + p.base + i * g.width); });
+        }
+        float d[8][8];
+        unroll<8>([&](auto i) {
+            unroll<8>([&](auto j) {
+                float qv;
+                if constexpr (kFast) {
+                    qv = i8_byte_f32(j < 4 ? q8[i].x : q8[i].y, j & 3);
+                } else {
+                    qv = qf[i][j];
+                }
+                d[i][j] = qv * qp.q.v[i * 8 + j];
+            });
+        });
+        idct_tile(T, d, [&](auto v, float (&r)[8]) {
+            unroll<8>([&](auto u) { r[u] = r[u] + 128.0f; });
+            uint2 r8;  // convertToUnsignedChar (utils.cu:21): clamp, truncate, packed
+            if constexpr (kStats || kRecon == kRtReconU8) {
+                r8 = make_uint2(pack_u8x4(r[0], r[1], r[2], r[3]), pack_u8x4(r[4], r[5], r[6], r[7]));
+            }
+            if constexpr (kStats) {
+                // integer sums on the packed bytes, 4 pixels per v_dot4_u32_u8:
+                // sum (x - r8)^2 = sum x^2 - 2 sum x.r8 + sum r8^2 (exact in uint32)
+                uint2 w;
+                if constexpr (kRaw == 0) {
+                    w = raw.r[v];
+                } else if constexpr (kRaw == 1) {
+                    w = again[v];
+                } else {
+                    w = stash[v * 64u + lane];
+                }
+                acc_xx = __builtin_amdgcn_udot4(w.x, w.x, acc_xx, false);
+                acc_xx = __builtin_amdgcn_udot4(w.y, w.y, acc_xx, false);
+                acc_xr = __builtin_amdgcn_udot4(w.x, r8.x, acc_xr, false);
+                acc_xr = __builtin_amdgcn_udot4(w.y, r8.y, acc_xr, false);
+                acc_rr = __builtin_amdgcn_udot4(r8.x, r8.x, acc_rr, false);
+                acc_rr = __builtin_amdgcn_udot4(r8.y, r8.y, acc_rr, false);
+                unroll<8>([&](auto u) {
+                    const float e = byte_f32(u < 4 ? w.x : w.y, u & 3) - r[u];
+                    acc_f = __builtin_fmaf(e, e, acc_f);
+                });
+            }
+            if constexpr (kRecon == kRtReconU8) {
+                st<true>(reinterpret_cast<uint2*>(static_cast<uint8_t*>(recon) + p.base + v * g.width), r8);
+            } else if constexpr (kRecon == kRtReconF32) {
+                rf32_sink(v, p, ok, seg, r);
+            }
+        });
+    });
+
+    if constexpr (kStats) {
+        // lanes without a tile (ragged last set, or waves past the end) hold zeros
+        unsigned long long f = static_cast<unsigned long long>(
+            __builtin_rintf(acc_f * kRtFixScale));  // < 2^24 * 2^16: exact in the convert
+        unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
+        unsigned long long xx = static_cast<unsigned long long>(acc_xx);
+        f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
+        __shared__ unsigned long long part[512 / 64][3];
+        const uint32_t w = threadIdx.x / 64u;
+        if ((threadIdx.x & 63u) == 0u) part[w][0] = f, part[w][1] = e8, part[w][2] = xx;
+        __syncthreads();
+        if (threadIdx.x < 3u) {
+            unsigned long long s = 0;
+            for (uint32_t k = 0; k < 512u / 64u; ++k) s += part[k][threadIdx.x];
+            if (s) atomicAdd(reinterpret_cast<unsigned long long*>(sums) + threadIdx.x, s);
+        }
+    }
+}
+
+inline dim3 roundtrip_grid(const TileGrid& g) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u;
+    return dim3((sets + 7u) / 8u);
+}
+
+namespace rt_detail {
+template <int kRecon, bool kStats, bool kFast>
+hipError_t go(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
+              hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kFast>), roundtrip_grid(g), dim3(512), 0, s, img, coef,
+                       recon, sums, g, qp);
+    return hipGetLastError();
+}
+template <int kRecon>
+hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
+                bool fast, hipStream_t s) {
+    if (sums) {
+        return fast ? go<kRecon, true, true>(img, coef, recon, sums, g, qp, s)
+                    : go<kRecon, true, false>(img, coef, recon, sums, g, qp, s);
+    }
+    return fast ? go<kRecon, false, true>(img, coef, recon, sums, g, qp, s)
+                : go<kRecon, false, false>(img, coef, recon, sums, g, qp, s);
+}
+}  // namespace rt_detail
+
+inline hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
+                                        RtSums* sums, const TileGrid& g, const QParams& qp, bool fast,
+                                        hipStream_t s) {
+    if (sums) {
+        const hipError_t e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);
+        if (e != hipSuccess) return e;
+    }
+    switch (recon_kind) {
+        case kRtReconU8: return rt_detail::go_r<kRtReconU8>(img, coef, recon, sums, g, qp, fast, s);
+        case kRtReconF32: return rt_detail::go_r<kRtReconF32>(img, coef, recon, sums, g, qp, fast, s);
+        default: return rt_detail::go_r<kRtReconNone>(img, coef, nullptr, sums, g, qp, fast, s);
+    }
+}
+
+}  // namespace hpdct

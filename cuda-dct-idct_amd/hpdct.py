@@ -49,6 +49,7 @@ C_SYMBOLS = [
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
+    "hpdct_roundtrip_u8",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -128,6 +129,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_stream_forward.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
     lib.hpdct_baseline_forward.restype = ctypes.c_int
+    lib.hpdct_roundtrip_u8.argtypes = [vp, vp, vp, ctypes.c_int, vp, i64, i64, vp]
+    lib.hpdct_roundtrip_u8.restype = ctypes.c_int
     for name, mangled in COMPAT_SYMBOLS.items():
         f = getattr(lib, mangled)
         f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp] + ([vp] if not name.endswith("_cuda") else [])
@@ -280,6 +283,68 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
         (FLAG_WRITEBACK_SHIFT if writeback_shift else 0)
     args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(dst.data_ptr()), _dtype_code(dst),
             h, w, None if transform is None else ctypes.c_void_p(transform.data_ptr()), flags, _stream_ptr(stream))
+
+    def call():
+        st = fn(*args)
+        if st:
+            _check(st)
+    return call
+
+
+SSE_F32_UNIT = 1.0 / 65536.0  # HPDCT_SSE_F32_UNIT
+
+
+def _roundtrip_args(image, coef, recon, sums_buf, height, width, stream):
+    for t in (image, coef) + ((recon,) if recon is not None else ()):
+        if not t.is_cuda or not t.is_contiguous():
+            raise HpdctError(1, "image, coefficients and reconstruction must be contiguous CUDA tensors")
+    if _dtype_code(image) != U8 or _dtype_code(coef) != F32:
+        raise HpdctError(2, "round trip: uint8 image -> float32 coefficients")
+    h, w = _hw(image, height, width)
+    return (ctypes.c_void_p(image.data_ptr()), ctypes.c_void_p(coef.data_ptr()),
+            None if recon is None else ctypes.c_void_p(recon.data_ptr()),
+            F32 if recon is None else _dtype_code(recon),
+            None if sums_buf is None else ctypes.c_void_p(sums_buf.data_ptr()), h, w, _stream_ptr(stream))
+
+
+def sums_from_buffer(sums_buf) -> dict:
+    """The 3 x uint64 device struct hpdct_roundtrip_sums (held in an int64
+    tensor) as {"sse_f32", "sse_u8", "sum_x2"} (synchronises)."""
+    v = [int(x) & ((1 << 64) - 1) for x in sums_buf.cpu().tolist()]
+    return {"sse_f32": v[0] * SSE_F32_UNIT, "sse_u8": v[1], "sum_x2": v[2]}
+
+
+def quality_from_sums(sums: dict, pixels: int) -> dict:
+    """PEEN (%) and MSE of both reconstructions from the round-trip sums
+    (PEEN = 100 sqrt(sse / sum x^2), MSE = sse / pixels; hpdct_quality.py)."""
+    sx = float(sums["sum_x2"])
+    return {"mse_f32": sums["sse_f32"] / pixels, "peen_f32_pct": 100.0 * (sums["sse_f32"] / sx) ** 0.5,
+            "mse_u8": sums["sse_u8"] / pixels, "peen_u8_pct": 100.0 * (sums["sse_u8"] / sx) ** 0.5}
+
+
+def roundtrip(image, coef=None, recon=None, *, recon_dtype=None, sums=False, height=None, width=None,
+              stream=None):
+    """One-pass C3 round trip on the GPU (hpdct_roundtrip_u8): uint8 frame ->
+    fp32 quantised coefficients, the reconstruction (uint8 clamp + truncate or
+    fp32, when recon or recon_dtype is given) and, with sums=True, the quality
+    sums.  Bit-identical to forward() followed by inverse().
+    Returns (coef, recon or None, sums dict or None); reading the sums
+    synchronises the stream."""
+    torch = _torch()
+    if coef is None:
+        coef = torch.empty(image.shape, dtype=torch.float32, device=image.device)
+    if recon is None and recon_dtype is not None:
+        recon = torch.empty(image.shape, dtype=recon_dtype, device=image.device)
+    sums_buf = torch.empty(3, dtype=torch.int64, device=image.device) if sums else None
+    _check(load_library().hpdct_roundtrip_u8(*_roundtrip_args(image, coef, recon, sums_buf, height, width, stream)))
+    return coef, recon, (sums_from_buffer(sums_buf) if sums else None)
+
+
+def bind_roundtrip(image, coef, recon=None, sums_buf=None, *, stream=None, height=None, width=None):
+    """Pre-resolved round-trip launch (like bind): a zero-argument callable.
+    sums_buf: an int64 CUDA tensor of 3 elements, or None."""
+    args = _roundtrip_args(image, coef, recon, sums_buf, height, width, stream)
+    fn = load_library().hpdct_roundtrip_u8
 
     def call():
         st = fn(*args)

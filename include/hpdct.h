@@ -18,6 +18,9 @@
  *   hpdct_inverse          idct_all_blocks_cuda     main_newAppr.cu:293-332
  *                          (multiply_matrices -> cuda_matrix_idct ->
  *                          add_matrix_scalar fused into one pass)
+ *   hpdct_roundtrip_u8     dct_all_blocks_cuda then idct_all_blocks_cuda
+ *                          (main_newAppr.cu:99,120) and the host-side
+ *                          PEEN/MSE of README.md:62-69, in one pass
  *   hpdct_forward(..., HPDCT_FLAG_ROW_FIRST)  dct_all_blocks  main_cublass_2.cu:197-252
  *   hpdct_inverse(..., HPDCT_FLAG_ROW_FIRST)  idct_all_blocks main_cublass_2.cu:257-311
  *   hpdct_set_quant_table  cudaMemcpyToSymbol(const_quant_matrix, ...)
@@ -122,6 +125,31 @@ hpdct_status hpdct_forward_u8_i8(const uint8_t* d_image, int8_t* d_coef, int64_t
 hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t height, int64_t width,
                                    void* stream);
 
+/* One-pass round trip (BASELINE config C3: forward DCT + IDCT with the
+ * PEEN/MSE check).  The reference runs dct_all_blocks_cuda then
+ * idct_all_blocks_cuda (main_newAppr.cu:99,120; benchmark_newAppr.cu:93,105)
+ * and measures quality on the host (README.md:62-69).  Here one kernel reads
+ * the uint8 frame once and writes
+ *   d_coef   fp32 quantised coefficients (required; as hpdct_forward U8 -> F32)
+ *   d_recon  the reconstruction R+128 as recon_type HPDCT_U8 (clamp +
+ *            truncate) or HPDCT_F32 (no clamp), or NULL for none (as
+ *            hpdct_inverse F32 -> recon_type on d_coef)
+ *   d_sums   device struct, or NULL: the quality sums below (overwritten)
+ * Built-in T, the library Q, level shift 128; coefficients and reconstruction
+ * are bit-identical to the two separate calls.  HBM traffic per pixel: 1 B
+ * read, 4 B (+1 or 4 B) written, against 10 B for the two calls.
+ * PEEN = 100 sqrt(sse / sum_x2) %, MSE = sse / (height*width) (the
+ * definitions of the README table). */
+typedef struct hpdct_roundtrip_sums {
+    uint64_t sse_f32_fx; /* sum (x - (R+128))^2 in units of 2^-16 (HPDCT_SSE_F32_UNIT): per-tile fp32
+                            partial sums, each rounded to the unit, added exactly */
+    uint64_t sse_u8;     /* sum (x - u8(R+128))^2, exact */
+    uint64_t sum_x2;     /* sum x^2, exact */
+} hpdct_roundtrip_sums;
+#define HPDCT_SSE_F32_UNIT (1.0 / 65536.0)
+hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
+                                hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream);
+
 /* Host-resident batch (BASELINE config C5): frame f (height x width uint8 at
  * h_frames[f]) -> coefficients at h_coef[f] (out_type HPDCT_F32 or HPDCT_I8),
  * pipelined over nstreams (1..16) HIP streams, each with one device input and
@@ -144,9 +172,11 @@ hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_
  * per program).  Output is bit-identical in every mapping; only speed differs.
  *   AUTO   per frame: eight lanes per 8x8 tile ("octet") for frames below
  *          8 x 64-tile sets per CU; above that two lanes per tile ("duo") for
- *          fp32 -> fp32, one lane per tile for the rest (DESIGN.md "Kernels").
+ *          fp32 -> fp32 and the fp32 -> uint8 inverse, one lane per tile for
+ *          the rest (DESIGN.md "Kernels").
  *   TILE   one lane per tile always.     OCTET  eight lanes per tile always.
- *   DUO    two lanes per tile for every fp32 -> fp32 kernel, AUTO otherwise.
+ *   DUO    two lanes per tile for every fp32 -> fp32 kernel and the fp32 -> uint8
+ *          inverse, AUTO otherwise.
  * The cublasDCTv2 pass order (HPDCT_FLAG_ROW_FIRST) runs two lanes per tile
  * (rows first) except under TILE.  Process-wide; the initial value comes from the environment variable
  * HPDCT_MAPPING ("auto", "tile", "octet", "duo"), else AUTO.  For A/B

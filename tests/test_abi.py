@@ -178,6 +178,25 @@ def test_bad_arguments_rejected(hp):
         hp.set_quant_table(None)
 
 
+def test_roundtrip_arguments_rejected(hp):
+    """hpdct_roundtrip_u8 validates before any device work (no GPU here)."""
+    L = hp.load_library()
+    a, b, c, s = (ctypes.c_void_p(1 << 20), ctypes.c_void_p(1 << 30), ctypes.c_void_p(1 << 31),
+                  ctypes.c_void_p(1 << 32))
+    rt = L.hpdct_roundtrip_u8
+    assert rt(a, b, c, hp.U8, s, 8, 12, None) == 1           # width not a multiple of 8
+    assert rt(None, b, c, hp.U8, s, 8, 8, None) == 1         # null image
+    assert rt(a, None, c, hp.U8, s, 8, 8, None) == 1         # null coefficients
+    assert rt(a, b, c, hp.I8, s, 8, 8, None) == 2            # int8 is not a reconstruction type
+    assert rt(a, ctypes.c_void_p((1 << 30) + 4), c, hp.U8, s, 8, 8, None) == 1  # misaligned coefficients
+    assert rt(a, b, c, hp.F32, ctypes.c_void_p((1 << 32) + 4), 8, 8, None) == 1  # misaligned sums
+    assert rt(a, ctypes.c_void_p((1 << 20) + 16), None, hp.U8, None, 8, 8, None) == 1  # image/coef overlap
+    assert rt(a, b, ctypes.c_void_p((1 << 30) + 64), hp.U8, None, 8, 8, None) == 1  # coef/recon overlap
+    assert rt(a, b, c, hp.U8, ctypes.c_void_p((1 << 31) + 8), 8, 8, None) == 1  # sums inside the recon
+    assert b"overlap" in L.hpdct_last_error_string()
+    assert ctypes.sizeof(ctypes.c_uint64 * 3) == 24  # hpdct_roundtrip_sums: three uint64
+
+
 def test_host_rand_matches_glibc(hp, oracle):
     assert np.array_equal(hp.fill_rand_u8(100000, 42), oracle.rand_u8(100000, 42))
     assert np.array_equal(hp.fill_rand_u8(5000, 7), oracle.rand_u8(5000, 7))

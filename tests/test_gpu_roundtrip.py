@@ -1,0 +1,183 @@
+"""GPU parity of the one-pass round trip (hpdct_roundtrip_u8, BASELINE config
+C3: forward DCT + IDCT with the PEEN/MSE check) against the CPU oracle.
+
+Bar: the coefficients and both reconstructions are BIT-EXACT to
+oracle.fdct / oracle.idct / oracle.to_u8 (convertToUnsignedChar) -- the same
+contract as the two separate kernels; sum_x2 and sse_u8 are exact integers;
+sse_f32 is a sum of per-tile fp32 partials, so it is checked to a relative
+REL_SSE_F32 of the float64 sum.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_SSE_F32 = 1e-6
+SHAPES = [(8, 8), (8, 16), (16, 8), (24, 40), (8, 4096), (520, 8), (1000, 1008), (72, 2056), (256, 256)]
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLD, "golden.json")) as fh:
+        return json.load(fh)
+
+
+def to_dev(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def to_host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def expected(oracle, img, Q=None):
+    q = oracle.fdct(img, Q=Q)
+    r = oracle.idct(q, Q=Q)
+    r8 = oracle.to_u8(r)
+    x = img.astype(np.float64)
+    sums = {"sum_x2": int((img.astype(np.int64) ** 2).sum()),
+            "sse_u8": int(((img.astype(np.int64) - r8.astype(np.int64)) ** 2).sum()),
+            "sse_f32": float(((x - r.astype(np.float64)) ** 2).sum())}
+    return q, r, r8, sums
+
+
+def check_sums(got, want):
+    assert got["sum_x2"] == want["sum_x2"]
+    assert got["sse_u8"] == want["sse_u8"]
+    assert abs(got["sse_f32"] - want["sse_f32"]) <= REL_SSE_F32 * max(want["sse_f32"], 1.0)
+
+
+@pytest.mark.parametrize("h,w", SHAPES)
+def test_roundtrip_shapes(hp, oracle, dev, h, w):
+    import torch
+    img = np.random.default_rng(h * 131 + w).integers(0, 256, (h, w), dtype=np.uint8)
+    q, r, r8, sums = expected(oracle, img)
+    x = to_dev(img, dev)
+    coef, rec8, got = hp.roundtrip(x, recon_dtype=torch.uint8, sums=True)
+    assert bits_equal(to_host(coef), q)
+    assert np.array_equal(to_host(rec8), r8)
+    check_sums(got, sums)
+    coef, recf, none = hp.roundtrip(x, recon_dtype=torch.float32, sums=False)
+    assert none is None
+    assert bits_equal(to_host(coef), q)
+    assert bits_equal(to_host(recf), r)
+
+
+def test_roundtrip_equals_two_kernels(hp, dev):
+    """Same bits as hpdct_forward + hpdct_inverse on the device."""
+    import torch
+    x = torch.empty((512, 1024), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=3)
+    q2 = hp.forward(x)
+    r2 = hp.inverse(q2, out_dtype=torch.uint8)
+    coef, rec, _ = hp.roundtrip(x, recon_dtype=torch.uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(coef.view(torch.int32), q2.view(torch.int32))
+    assert torch.equal(rec, r2)
+
+
+def test_roundtrip_sums_only_and_no_sums(hp, oracle, dev):
+    img = oracle.rand_u8(64 * 128, 5).reshape(64, 128)
+    q, _, _, sums = expected(oracle, img)
+    coef, rec, got = hp.roundtrip(to_dev(img, dev), recon_dtype=None, sums=True)
+    assert rec is None
+    assert bits_equal(to_host(coef), q)
+    check_sums(got, sums)
+    coef, rec, got = hp.roundtrip(to_dev(img, dev), recon_dtype=None, sums=False)
+    assert got is None and rec is None
+    assert bits_equal(to_host(coef), q)
+
+
+@pytest.mark.parametrize("qtab", ["jpeg_q90", "fractional", "ones", "max255", "large"])
+def test_roundtrip_quant_tables(hp, oracle, dev, qtab):
+    """Integer tables in 1..255 whose quotients fit int8 take the packed fast
+    path; every other table (fractional, all-ones, > 255) the general one."""
+    import torch
+    rng = np.random.default_rng(17)
+    base = oracle.default_quant()
+    Q = {"jpeg_q90": np.clip(np.floor((base * 20 + 50) / 100), 1, 255),
+         "fractional": rng.uniform(1.0, 50.0, (8, 8)),
+         "ones": np.ones((8, 8)),
+         "max255": np.full((8, 8), 255.0),
+         "large": rng.integers(200, 5000, (8, 8))}[qtab].astype(np.float32)
+    img = rng.integers(0, 256, (64, 192), dtype=np.uint8)
+    q, r, r8, sums = expected(oracle, img, Q=Q)
+    hp.set_quant_table(Q)
+    try:
+        coef, rec8, got = hp.roundtrip(to_dev(img, dev), recon_dtype=torch.uint8, sums=True)
+        _, recf, _ = hp.roundtrip(to_dev(img, dev), recon_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        hp.set_quant_table(None)
+    assert bits_equal(to_host(coef), q)
+    assert np.array_equal(to_host(rec8), r8)
+    assert bits_equal(to_host(recf), r)
+    check_sums(got, sums)
+
+
+def test_roundtrip_extremes(hp, oracle, dev):
+    """All-0 / all-255 / sign-pattern tiles: the largest |q| and the most
+    clamping in the uint8 reconstruction."""
+    import torch
+    t = oracle.default_transform()
+    tiles = []
+    for v in range(8):
+        for u in range(8):
+            s = np.sign(np.outer(t[v], t[u]))
+            tiles.append(np.where(s > 0, 255, 0))
+            tiles.append(np.where(s > 0, 0, 255))
+    tiles += [np.zeros((8, 8)), np.full((8, 8), 255), np.full((8, 8), 128)]
+    img = np.ascontiguousarray(np.concatenate(tiles, axis=1).astype(np.uint8))
+    q, r, r8, sums = expected(oracle, img)
+    coef, rec8, got = hp.roundtrip(to_dev(img, dev), recon_dtype=torch.uint8, sums=True)
+    assert bits_equal(to_host(coef), q)
+    assert np.array_equal(to_host(rec8), r8)
+    check_sums(got, sums)
+
+
+def test_roundtrip_rejects_bad_arguments(hp, dev):
+    import torch
+    x = torch.zeros((16, 16), dtype=torch.uint8, device=dev)
+    with pytest.raises(hp.HpdctError):
+        hp.roundtrip(x[:, :12].contiguous())  # width not a multiple of 8
+    buf = torch.zeros(16 * 16 + 4, dtype=torch.float32, device=dev)
+    with pytest.raises(hp.HpdctError):
+        hp.roundtrip(x, coef=buf[1:257].view(16, 16))  # misaligned coefficient plane
+
+
+def test_c3_8192_roundtrip_one_pass(hp, oracle, dev, golden):
+    """C3 at full size: coefficients and fp32 reconstruction match the golden
+    digests of the oracle; PEEN/MSE from the device sums match the golden
+    values of both reconstructions."""
+    import torch
+    g = golden["configs"]["c3_8192"]
+    img = oracle.rand_u8(8192 * 8192).reshape(8192, 8192)
+    x = to_dev(img, dev)
+    coef, recf, got = hp.roundtrip(x, recon_dtype=torch.float32, sums=True)
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    assert sha(to_host(coef)) == g["q_f32_sha256"]
+    assert sha(to_host(recf)) == g["roundtrip_f32_sha256"]
+    px = 8192 * 8192
+    q = hp.quality_from_sums(got, px)
+    assert abs(q["mse_f32"] - g["mse_f32"]) < 1e-5 * g["mse_f32"]
+    assert abs(q["peen_f32_pct"] - g["peen_f32"]) < 1e-5 * g["peen_f32"]
+    assert abs(q["mse_u8"] - g["mse_u8"]) < 1e-9 * g["mse_u8"]
+    assert abs(q["peen_u8_pct"] - g["peen_u8"]) < 1e-9 * g["peen_u8"]
+    assert got["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
