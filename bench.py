@@ -304,7 +304,7 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
             "two_kernels": {"ms_per_frame": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
                             "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
-            "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world),
+            "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums", n),
                              quality_from_device_sums=qd,
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums, one "
                                   "kernel; bit-identical to the two kernels"),

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Turn the rocprofv3 PMC passes of tools/pmc_traffic.sh into per-launch HBM
 bytes for the path's kernels (profiles/pmc_traffic.json): the headline
-u8 -> fp32 kernel, the int8 forward and the fp32 duo forward / inverse.
+u8 -> fp32 kernel, the int8 forward, the fp32 duo forward / inverse, the
+fp32 -> u8 duo inverse and the one-pass round trip.
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB per dispatch.  Each is scaled by
 the ratio (known bytes / counted bytes) measured on a calibration kernel of
@@ -42,12 +43,15 @@ def pick(d, needle, exclude=()):
     raise KeyError(needle)
 
 
-# kernel key -> (name needle, exclude, read width, write width, B/px read, B/px written)
+# kernel key -> (name needle, exclude, read width, write width, B/px read, B/px written); a write
+# width may be a {width: B/px} mix, calibrated per part (the round trip stores fp32 rows and u8 rows)
 KERNELS = {
     "fdct_u8_f32": ("fdct_kernel<unsigned char, float, true, true, false", (), "x2", "x4nt", 1, 4),
     "fdct_u8_i8": ("fdct_kernel<unsigned char, signed char, true, true, false", (), "x2", "x2nt", 1, 1),
     "fdct_f32_f32_duo_runtimeT": ("fdct_duo_kernel<true, false, false", (), "x4", "x4nt", 4, 4),
-    "idct_f32_f32_duo": ("idct_duo_kernel<true, true", (), "x4", "x4nt", 4, 4),
+    "idct_f32_f32_duo": ("idct_duo_kernel<true, true", ("unsigned char",), "x4", "x4nt", 4, 4),
+    "idct_f32_u8_duo": ("idct_duo_kernel<true, true, 8208u, unsigned char>", (), "x4", "x2nt", 4, 1),
+    "roundtrip_u8_f32_u8_sums": ("roundtrip_kernel<1, true, true, 2>", (), "x2", {"x4nt": 4, "x2nt": 1}, 1, 5),
 }
 
 
@@ -78,7 +82,11 @@ def main():
         except KeyError:
             continue
         read_b = kf * 1024 * scale[rw]
-        write_b = kw * 1024 * scale[ww]
+        if isinstance(ww, dict):  # bytes-weighted mean of the parts' calibration scales
+            write_b = kw * 1024 * sum(scale[w] * b for w, b in ww.items()) / sum(ww.values())
+            ww = "+".join(ww)
+        else:
+            write_b = kw * 1024 * scale[ww]
         alg = (rb + wb) * n * n
         kernels[key] = {
             "size": n,
