@@ -1,4 +1,5 @@
-// hpdct_inv.hip -- inverse kernels, fp32 coefficients in (int8 in: hpdct_inv_i8.hip).  Kernels: hpdct_kernels_impl.hpp.
+// hpdct_inv_i8.hip -- inverse kernels, int8 coefficients in (split from
+// hpdct_inv.hip so the two halves compile in parallel).  Kernels: hpdct_kernels_impl.hpp.
 #include "hpdct_launch.hpp"
 
 namespace hpdct {
@@ -9,8 +10,8 @@ namespace hpdct {
         return launch_idct_impl<TI, TO, DQ, BT>(a, b, w, g, t, q, sh, rf, s);                               \
     }
 #define HPDCT_INV_T(TI, TO, DQ) HPDCT_INV(TI, TO, DQ, true) HPDCT_INV(TI, TO, DQ, false)
-HPDCT_INV_T(float, float, true)
-HPDCT_INV_T(float, float, false)
-HPDCT_INV_T(float, uint8_t, true)
-HPDCT_INV_T(float, uint8_t, false)
+HPDCT_INV_T(int8_t, float, true)
+HPDCT_INV_T(int8_t, float, false)
+HPDCT_INV_T(int8_t, uint8_t, true)
+HPDCT_INV_T(int8_t, uint8_t, false)
 }  // namespace hpdct
