@@ -242,7 +242,7 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
     if True:
         steps = max(10, args.steps // 2)
         # fp32 in -> fp32 out (the reference's own data types; compat kernel)
-        f32_in = [imgs[s].float() for s in range(min(2, args.sets))]
+        f32_in = [imgs[s].float() for s in range(args.sets)]
         f32_out = outs[:len(f32_in)]
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, stream=stream) for i in range(len(f32_in))]

@@ -102,6 +102,30 @@ def test_roundtrip_sums_only_and_no_sums(hp, oracle, dev):
     assert bits_equal(to_host(coef), q)
 
 
+def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
+    """The sums are written (not accumulated) by each launch: the library's
+    per-stream accumulator is re-zeroed by the last workgroup, so back-to-back
+    launches of different grid sizes, a garbage-filled sums buffer, and
+    launches on a second stream all give this frame's totals."""
+    import torch
+    a = oracle.rand_u8(64 * 128, 11).reshape(64, 128)
+    b = oracle.rand_u8(520 * 1008, 12).reshape(520, 1008)
+    want_a, want_b = expected(oracle, a)[3], expected(oracle, b)[3]
+    xa, xb = to_dev(a, dev), to_dev(b, dev)
+    side = torch.cuda.Stream(device=dev)
+    bufs = []
+    for i, (x, strm) in enumerate([(xa, None), (xb, None), (xa, side), (xa, None), (xb, side), (xb, side),
+                                    (xa, None)]):
+        buf = torch.full((3,), -1234567, dtype=torch.int64, device=dev)
+        coef = torch.empty(x.shape, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        hp.bind_roundtrip(x, coef, None, buf, stream=side if strm is side else None)()
+        bufs.append((buf, want_a if x is xa else want_b))
+    torch.cuda.synchronize()
+    for buf, want in bufs:
+        check_sums(hp.sums_from_buffer(buf), want)
+
+
 @pytest.mark.parametrize("qtab", ["jpeg_q90", "fractional", "ones", "max255", "large"])
 def test_roundtrip_quant_tables(hp, oracle, dev, qtab):
     """Integer tables in 1..255 whose quotients fit int8 take the packed fast
