@@ -323,6 +323,23 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         line["note"] = "cache-resident (40 MB working set < 256 MiB MALL): hbm_frac not meaningful"
         extras["c2_fwd_u8_f32"] = line
         del c2_in, c2_out
+        # C2 frames batched: a 1024^2 frame is 256 tile sets, one per CU, so a
+        # single-frame launch is dominated by the per-dispatch cost (~4 us; a
+        # HIP graph of the same launches does not remove it,
+        # profiles/r01/c2_probe.log).  32 frames stacked as one (32*1024) x 1024
+        # image (the C-ABI's batch layout) make one launch; 2 sets of 160 MB
+        nb = 32
+        c2b_in = [torch.empty((nb * c2, c2), dtype=torch.uint8, device=dev) for _ in range(2)]
+        for s, t in enumerate(c2b_in):
+            hpdct.fill_hash_u8(t, seed=4242 + s)
+        c2b_out = [torch.empty((nb * c2, c2), dtype=torch.float32, device=dev) for _ in range(2)]
+        calls = [hpdct.bind("fwd", c2b_in[s], c2b_out[s], stream=stream) for s in range(2)]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        line = _line(nb * c2 * c2, rms / steps, float(k.mean()), BYTES_PER_PX["u8_f32"], world)
+        line["us_per_frame"] = round(rms / steps / nb * 1e3, 3)
+        line["note"] = f"{nb} 1024^2 frames per launch, stacked (C-ABI batch layout)"
+        extras["c2_batched_fwd_u8_f32"] = line
+        del c2b_in, c2b_out
         torch.cuda.empty_cache()
         if not args.no_c4c5:
             extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks)

@@ -62,6 +62,8 @@ enum : unsigned {
     kVarPrio = 1u << 26,        // s_setprio 3 while the wave computes its addresses and issues its loads
     // diagnostics only (tools/kbench): split the kernel's time into its phases
     kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
+    kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
+                                // over the 8 XCDs; remap so XCD x walks one contiguous 1/8 of the sets
     kVarNoStore = 1u << 28,     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
 };
 template <unsigned kVar>
@@ -393,7 +395,13 @@ template <unsigned kVar, typename TIn, typename Body>
 __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, float4* slots, Body&& body) {
     constexpr bool kPersist = (kVar & kVarPersist) != 0;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
+    uint32_t block = blockIdx.x;
+    if constexpr ((kVar & kVarXcdSwz) != 0) {
+        // bijective: XCD x = block % 8 owns q (+1 for x < r) consecutive blocks
+        const uint32_t nb = gridDim.x, q = nb / 8u, r = nb % 8u, x = block % 8u;
+        block = x * q + (x < r ? x : r) + block / 8u;
+    }
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(block * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t nsets = (g.ntiles + 63u) / 64u;
     auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) {
         const uint32_t t0 = set * 64u;

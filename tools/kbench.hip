@@ -372,6 +372,8 @@ int main(int argc, char** argv) {
         {"u8->f32 tile st sc0sc1", launch_var<(B & ~N) | W512 | kVarStSc0Sc1>},
         {"u8->f32 tile plain st", launch_var<(B & ~N) | W512>},
         {"u8->f32 octet", launch_fwd_oct<uint8_t, float, F | N | OR>},
+        {"u8->f32 tile xcd-swz", launch_var<B | W512 | kVarXcdSwz>},
+        {"u8->f32 tile (product)", launch_var<B | W512>},
     };
     // pairs (2k, 2k+1), checked bit-exact against each other
     std::vector<Variant> other = {
@@ -409,6 +411,10 @@ int main(int argc, char** argv) {
         {"fwd u8->i8 octet", launch_fwd_oct<uint8_t, int8_t, F | N>},
         {"inv i8->u8 tile", launch_inv_any<int8_t, uint8_t, N | W512>},
         {"inv i8->u8 octet", launch_inv_oct<int8_t, uint8_t, N>},
+        {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
+        {"fwd u8->i8 tile xcd-swz", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP | kVarXcdSwz>},
+        {"inv i8->u8 tile", launch_inv_any<int8_t, uint8_t, N | W512>},
+        {"inv i8->u8 tile xcd-swz", launch_inv_any<int8_t, uint8_t, N | W512 | kVarXcdSwz>},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);
