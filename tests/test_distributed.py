@@ -80,7 +80,10 @@ def _worker(rank, world, port, height, width, result_path, wire_int8=False):
 
 
 @pytest.mark.parametrize("world,height,width,wire", [(2, 64, 96, False), (2, 72, 40, False), (3, 80, 64, False),
-                                                     (2, 64, 96, True), (3, 72, 16, True)])
+                                                     (2, 64, 96, True), (3, 72, 16, True),
+                                                     # the node size of the C4 run: uniform slabs (gather) and
+                                                     # ragged slabs (send/recv fan-in)
+                                                     (8, 128, 64, False), (8, 136, 32, True)])
 def test_sharded_gather_equals_unsharded(tmp_path, world, height, width, wire):
     import torch.multiprocessing as mp
     result = tmp_path / "result.txt"
