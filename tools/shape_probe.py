@@ -1,0 +1,47 @@
+"""Frame-shape probe (development tool, not the product): forward u8 -> fp32
+time per 64 Mpx for frames of the same pixel count and different widths, to
+see whether the row stride matters.  Usage: python tools/shape_probe.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-dct-idct_amd"))
+
+import torch  # noqa: E402
+import hpdct  # noqa: E402
+
+
+def us_per_launch(calls, steps=80, warmup=8):
+    for i in range(warmup):
+        calls[i % len(calls)]()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for i in range(steps):
+        calls[i % len(calls)]()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps * 1e3
+
+
+def main():
+    dev = torch.device("cuda:0")
+    hpdct.load_library()
+    shapes = [(8192, 8192), (4096, 16384), (2048, 32768), (16384, 4096), (8192, 8200), (4096, 16392),
+              (16384, 16384), (2048, 16384), (2048, 16392)]
+    for h, w in shapes:
+        sets = 4
+        ins = [torch.empty((h, w), dtype=torch.uint8, device=dev) for _ in range(sets)]
+        for s, t in enumerate(ins):
+            hpdct.fill_hash_u8(t, seed=s)
+        outs = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in range(sets)]
+        us = us_per_launch([hpdct.bind("fwd", ins[s], outs[s]) for s in range(sets)])
+        px = h * w
+        print(f"{h:6d} x {w:6d}  {us:9.2f} us  {us * 64 * 2**20 / px:8.2f} us per 64 Mpx  "
+              f"{5 * px / us / 1e6:7.3f} TB/s", flush=True)
+        del ins, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
