@@ -64,7 +64,11 @@ enum : unsigned {
     kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
     kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
                                 // over the 8 XCDs; remap so XCD x walks one contiguous 1/8 of the sets
-    kVarNoStore = 1u << 28,     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
+    kVarNoStore = 1u << 28,
+    kVarStraddle = 1u << 30,    // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
+                                // multiple of 512 px) stores two contiguous runs per instruction instead of
+                                // 32 B per lane; launched only for such widths (the branch costs the
+                                // power-of-two frames ~3 %, profiles/r01/ab_straddle.log)     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
 };
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
@@ -387,10 +391,31 @@ __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* 
     st_pol<kNT, kPol>(seg, 16u * (64u + sw(lane)), b);
 }
 
+// The same for a set that straddles a tile-row boundary (ragged widths): its
+// first k tiles end tile row ty (row segment at seg), the other 64-k start
+// tile row ty+1 (at seg2).  Each store instruction then writes two contiguous
+// runs instead of falling back to one 32-B store per lane.
+template <bool kNT>
+__device__ __forceinline__ void store_row_lds2(float4* __restrict__ slot, float* __restrict__ seg,
+                                               float* __restrict__ seg2, uint32_t k, uint32_t lane,
+                                               const float (&c)[8]) {
+    slot[2 * lane] = make_float4(c[0], c[1], c[2], c[3]);
+    slot[2 * lane + 1] = make_float4(c[4], c[5], c[6], c[7]);
+    const float4 a = slot[lane];
+    const float4 b = slot[64 + lane];
+    // float4 q holds half q%2 of tile q/2's row: tiles < k go to seg, the rest to seg2
+    const uint32_t q0 = lane, q1 = 64u + lane, h = 2u * k;
+    st<kNT>(reinterpret_cast<float4*>(q0 < h ? seg + 4u * q0 : seg2 + 4u * (q0 - h)), a);
+    st<kNT>(reinterpret_cast<float4*>(q1 < h ? seg + 4u * q1 : seg2 + 4u * (q1 - h)), b);
+}
+
 // Per-wave walk over 64-tile sets: one set per wave (plain), or a grid-stride
 // loop with the next set's loads issued before the current set's compute.
-// body(raw, p, seg_ok, seg): seg_ok (wave-uniform) says the whole set is 64
-// valid tiles of one tile row, whose row segments start at element seg.
+// body(raw, p, split, seg): split (wave-uniform) = 64 when the whole set is 64
+// valid tiles of one tile row, whose row segments start at element seg; k in
+// 1..63 when the set is 64 valid tiles whose first k end one tile row (at seg)
+// and whose other 64-k start the next (RowSink derives that segment); 0 for a
+// ragged last set or a set over more than two tile rows (per-lane stores).
 template <unsigned kVar, typename TIn, typename Body>
 __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, float4* slots, Body&& body) {
     constexpr bool kPersist = (kVar & kVarPersist) != 0;
@@ -403,11 +428,25 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
     }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(block * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t nsets = (g.ntiles + 63u) / 64u;
-    auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) {
+    auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) -> uint32_t {
         const uint32_t t0 = set * 64u;
-        const bool ok = t0 + 63u < g.ntiles && (t0 / g.tiles_x) == ((t0 + 63u) / g.tiles_x);
-        seg = p.base - 8u * static_cast<uint64_t>(lane);
-        return ok;
+        if constexpr ((kVar & kVarStraddle) == 0) {
+            const bool ok = t0 + 63u < g.ntiles && (t0 / g.tiles_x) == ((t0 + 63u) / g.tiles_x);
+            seg = p.base - 8u * static_cast<uint64_t>(lane);
+            return ok ? 64u : 0u;
+        }
+        if (t0 + 63u >= g.ntiles) {
+            seg = 0;
+            return 0u;
+        }
+        const uint32_t ty0 = t0 / g.tiles_x, tx0 = t0 - ty0 * g.tiles_x;
+        const uint32_t k = g.tiles_x - tx0;  // tiles of the set left in tile row ty0
+        if (k >= 64u) {
+            seg = p.base - 8u * static_cast<uint64_t>(lane);
+            return 64u;
+        }
+        seg = static_cast<uint64_t>(ty0) * 8u * g.width + static_cast<uint64_t>(tx0) * 8u;
+        return 64u - k <= g.tiles_x ? k : 0u;
     };
     if constexpr ((kVar & kVarTwoSets) != 0) {
         const uint32_t s0 = wave * 2u;
@@ -421,7 +460,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         a.load(src + pa.base, g.width);
         b.load(src + pb.base, g.width);
         uint64_t seg;
-        bool ok = seg_info(s0, pa, seg);
+        uint32_t ok = seg_info(s0, pa, seg);
         body(a, pa, ok, seg);
         if (s0 + 1u < nsets) {  // wave-uniform
             ok = seg_info(s0 + 1u, pb, seg);
@@ -452,7 +491,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
             if (t >= g.ntiles) t = g.ntiles - 1u;
             const TilePos p = tile_pos(g, t);
             uint64_t seg;
-            const bool ok = seg_info(set, p, seg);
+            const uint32_t ok = seg_info(set, p, seg);
             body(cur, p, ok, seg);
             if (!more) break;
             cur = nxt;
@@ -463,7 +502,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(3);
         const TilePos p = tile_pos(g, wave * 64u + lane);
         uint64_t seg;
-        const bool ok = seg_info(wave, p, seg);
+        const uint32_t ok = seg_info(wave, p, seg);
         if (!p.valid) return;
         RawTile<TIn> raw;
         if constexpr ((kVar & kVarNoLoad) != 0 && sizeof(TIn) == 1) {
@@ -471,7 +510,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
                 raw.r[i] = make_uint2((lane * 0x01010101u) ^ (i * 0x10325476u), (lane * 0x03050709u) + i);
             });
         } else if constexpr ((kVar & kVarLdsLoad) != 0 && std::is_same_v<TIn, float>) {
-            if (ok) {
+            if (ok == 64u) {
                 raw.load_staged(src + seg, g.width, lane, slots);
             } else {
                 raw.load(src + p.base, g.width);
@@ -500,7 +539,7 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
                 if (np.valid) nxt.load(src + np.base, g.width);
             }
             uint64_t seg;
-            const bool ok = seg_info(set, p, seg);
+            const uint32_t ok = seg_info(set, p, seg);
             if (p.valid) body(cur, p, ok, seg);
             if (!more) break;
             cur = nxt;
@@ -521,13 +560,20 @@ struct RowSink {
     float4* slots;  // this wave's 2 x 128 float4 LDS slots (kLds)
 
     template <typename V>
-    __device__ __forceinline__ void operator()(V v, const TilePos& p, bool seg_ok, uint64_t seg,
+    __device__ __forceinline__ void operator()(V v, const TilePos& p, uint32_t split, uint64_t seg,
                                                const float (&c)[8]) const {
         if constexpr (kLds) {
-            if (seg_ok) {
+            if (split == 64u) {
                 constexpr int kPol = (kVar & kVarStSc1) ? 1 : (kVar & kVarStSc0Sc1) ? 2 : 0;
                 store_row_lds<kNT, (kVar & kVarLdsSwz) != 0, kPol>(slots + (v & 1) * 128,
                                                                    plane + seg + v * width, threadIdx.x & 63u, c);
+                return;
+            }
+            if ((kVar & kVarStraddle) != 0 && split != 0u) {
+                // next tile row's first tile: seg - (width - 8k) + 8 width (dense pitch: tiles_x = width / 8)
+                const uint64_t seg2 = seg + 7u * width + 8u * split;
+                store_row_lds2<kNT>(slots + (v & 1) * 128, plane + seg + v * width, plane + seg2 + v * width, split,
+                                    threadIdx.x & 63u, c);
                 return;
             }
         }
@@ -577,7 +623,7 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     const RowSink<kVar, float> wb_sink{shifted, g.width, slots};
 
-    walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok,
                                                       uint64_t seg) {
         if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && kBuiltinT && kQuant &&
                       !kWriteback && (kVar & kVarRowFirst) == 0) {
@@ -677,7 +723,7 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(con
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     const RowSink<kVar, float> dq_sink{dq_out, g.width, slots};
 
-    walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, bool ok,
+    walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok,
                                                        uint64_t seg) {
         float d[8][8];
         raw.to_float(d, 0.0f);

@@ -147,6 +147,20 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
         return fdct_octet_go<kOct, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift,
                                                                              s);
     }
+    // uint8 -> fp32 rows at a width that is not a multiple of 512 px: the
+    // straddle-capable variant (two-run staged stores, kVarStraddle)
+    constexpr bool kStraddleOk = std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float> && kBuiltinT;
+    if constexpr (kStraddleOk) {
+        if (g.tiles_x % 64u != 0u) {
+            if constexpr (kFastDivOk) {
+                if (fastdiv)
+                    return fdct_go<kBase | kVarFastDiv | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+                        img, out, shifted, g, t_dev, q, shift, s);
+            }
+            return fdct_go<kBase | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
+                                                                                           t_dev, q, shift, s);
+        }
+    }
     if constexpr (kFastDivOk) {
         if (fastdiv)
             return fdct_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
@@ -227,6 +241,11 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
         if (dq_out)
             return idct_go<kV | kVarWbDequant, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
                                                                                s);
+    }
+    if constexpr (std::is_same_v<TIn, int8_t> && std::is_same_v<TOut, float> && kBuiltinT) {
+        if (g.tiles_x % 64u != 0u)  // straddling sets: two-run staged stores (kVarStraddle)
+            return idct_go<kV | kVarStraddle, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift,
+                                                                              s);
     }
     return idct_go<kV, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
 }

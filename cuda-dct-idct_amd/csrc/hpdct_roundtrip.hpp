@@ -60,13 +60,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // profiles/r01/mappings/kbench2_rt.log)
 template <int kRecon>
 constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
-template <int kRecon, bool kStats, bool kFast, int kRaw = 2>
+template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false>
 __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
                                                                           RtSums* __restrict__ sums, TileGrid g,
                                                                           QParams qp) {
-    constexpr unsigned kVar = (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u);
+    constexpr unsigned kVar =
+        (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) | (kStraddle ? kVarStraddle : 0u);
     const TSource<true, true> T(nullptr);  // built-in T; u8 pixels and int8-range q are finite
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, float> coef_sink{coef, g.width, slots};
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
     }
     const uint32_t lane = threadIdx.x & 63u;
 
-    walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, bool ok, uint64_t seg) {
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         if constexpr (kStats && kRaw == 2) unroll<8>([&](auto i) { stash[i * 64u + lane] = raw.r[i]; });
         float x[8][8];
         raw.to_float_minus128(x);  // sub_matrix_scalar (utils_kernels.cu:16), exact: (int8)(b ^ 0x80)
@@ -185,6 +186,13 @@ namespace rt_detail {
 template <int kRecon, bool kStats, bool kFast>
 hipError_t go(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
               hipStream_t s) {
+    if constexpr (kFast) {
+        if (g.tiles_x % 64u != 0u) {  // straddling sets: two-run staged stores (kVarStraddle)
+            hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kFast, 2, true>), roundtrip_grid(g), dim3(512), 0, s,
+                               img, coef, recon, sums, g, qp);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kFast>), roundtrip_grid(g), dim3(512), 0, s, img, coef,
                        recon, sums, g, qp);
     return hipGetLastError();

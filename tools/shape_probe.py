@@ -29,6 +29,12 @@ def main():
     hpdct.load_library()
     shapes = [(8192, 8192), (4096, 16384), (2048, 32768), (16384, 4096), (8192, 8200), (4096, 16392),
               (16384, 16384), (2048, 16384), (2048, 16392)]
+    if len(sys.argv) > 1 and sys.argv[1] == "video":
+        # common video widths (not multiples of 512 px) against power-of-2 neighbours
+        shapes = [(32768, 1024), (32768, 1280), (16384, 1920), (16384, 2048), (8192, 3840), (8192, 4096),
+                  (4320, 7680), (4096, 8192)]
+    if len(sys.argv) > 1 and sys.argv[1] == "ab":
+        shapes = [(8192, 8192), (2048, 16384), (16384, 1920), (32768, 1280), (8192, 8200)]
     for h, w in shapes:
         sets = 4
         ins = [torch.empty((h, w), dtype=torch.uint8, device=dev) for _ in range(sets)]
