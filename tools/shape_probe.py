@@ -35,6 +35,26 @@ def main():
                   (4320, 7680), (4096, 8192)]
     if len(sys.argv) > 1 and sys.argv[1] == "ab":
         shapes = [(8192, 8192), (2048, 16384), (16384, 1920), (32768, 1280), (8192, 8200)]
+    if len(sys.argv) > 1 and sys.argv[1] == "f32":
+        # fp32 -> fp32 forward with the caller's T (the compat path's kernel) and
+        # the fp32 inverse, power-of-two vs video widths
+        T = torch.from_numpy(hpdct.default_transform()).to(dev)
+        for h, w in [(32768, 1024), (32768, 1280), (16384, 2048), (16384, 1920), (8192, 4096), (8192, 3840),
+                     (8192, 8192), (8192, 8200)]:
+            ins = [torch.empty((h, w), dtype=torch.uint8, device=dev) for _ in range(4)]
+            for s_, t in enumerate(ins):
+                hpdct.fill_hash_u8(t, seed=s_)
+            f32 = [t.float() for t in ins]
+            del ins
+            outs = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in range(4)]
+            fw = us_per_launch([hpdct.bind("fwd", f32[s_], outs[s_], transform=T) for s_ in range(4)])
+            iv = us_per_launch([hpdct.bind("inv", outs[s_], f32[s_]) for s_ in range(4)])
+            px = h * w
+            print(f"{h:6d} x {w:6d}  fwd f32 runtime-T {fw * 64 * 2**20 / px:8.2f}  inv f32 {iv * 64 * 2**20 / px:8.2f}"
+                  "  us per 64 Mpx", flush=True)
+            del f32, outs
+            torch.cuda.empty_cache()
+        return
     for h, w in shapes:
         sets = 4
         ins = [torch.empty((h, w), dtype=torch.uint8, device=dev) for _ in range(sets)]
