@@ -65,6 +65,8 @@ enum : unsigned {
     kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
                                 // over the 8 XCDs; remap so XCD x walks one contiguous 1/8 of the sets
     kVarNoStore = 1u << 28,
+    kVarPanel = 1u << 31,       // wide frames (tiles_x a multiple of 512, > 512): sets walk 4096-px-wide
+                                // column panels top to bottom, panel after panel, instead of whole rows
     kVarStraddle = 1u << 30,    // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
                                 // multiple of 512 px) stores two contiguous runs per instruction instead of
                                 // 32 B per lane; launched only for such widths (the branch costs the
@@ -500,9 +502,24 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
     } else if constexpr (!kPersist) {
         if (wave >= nsets) return;
         if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(3);
-        const TilePos p = tile_pos(g, wave * 64u + lane);
+        TilePos p;
         uint64_t seg;
-        const uint32_t ok = seg_info(wave, p, seg);
+        uint32_t ok;
+        constexpr uint32_t kPanelTiles = 512u;
+        if ((kVar & kVarPanel) != 0 && g.tiles_x % kPanelTiles == 0u && g.tiles_x > kPanelTiles) {
+            // set -> (panel, tile row, 64-tile chunk): every set is 64 tiles of one tile row
+            constexpr uint32_t kSpr = kPanelTiles / 64u;
+            const uint32_t per_panel = kSpr * (g.ntiles / g.tiles_x);
+            const uint32_t pn = wave / per_panel, r = wave - pn * per_panel;
+            const uint32_t ty = r / kSpr, cx = r - ty * kSpr;
+            p.valid = true;
+            seg = static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(pn * kPanelTiles + cx * 64u) * 8u;
+            p.base = seg + 8u * static_cast<uint64_t>(lane);
+            ok = 64u;
+        } else {
+            p = tile_pos(g, wave * 64u + lane);
+            ok = seg_info(wave, p, seg);
+        }
         if (!p.valid) return;
         RawTile<TIn> raw;
         if constexpr ((kVar & kVarNoLoad) != 0 && sizeof(TIn) == 1) {

@@ -83,6 +83,15 @@ void i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        128.0f);
 }
 
+// ---- forward u8 -> fp32 (the headline kernel), set order A/B on wide frames
+template <unsigned kVar>
+void f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp,
+                       128.0f);
+}
+
 // ---- round trip u8 -> fp32 coefficients + reconstruction (+ sums) ---------
 // the coefficient plane of set s is g_coef2[s] (found from the input pointer)
 std::vector<uint8_t*> g_img;
@@ -185,6 +194,9 @@ int main(int argc, char** argv) {
         {"rt", "rt fused sums only (5 B/px)", rt_fused<kRtReconNone, true, true>, false},
         {"rt", "rt fused f32 recon + sums (9 B/px)", rt_fused<kRtReconF32, true, true>, false},
         {"rt", "rt fused u8 recon + sums, IEEE/fp32 q", rt_fused<kRtReconU8, true, false>, true},
+        {"wide", "fwd u8->f32 tile (product)", f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"wide", "fwd u8->f32 tile panel 4096 px", f32_fwd<kProdVar<uint8_t, float> | F | kVarPanel>, true},
+        {"wide", "fwd u8->f32 tile (product) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | kVarNoStore>, false},
         {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | kVarNoLoad | kVarNoStore>, false},
@@ -197,10 +209,11 @@ int main(int argc, char** argv) {
     };
     // correctness: each variant against its group's first entry, on set 1
     {
-        std::vector<uint8_t> ref(px), got(px);
+        std::vector<uint8_t> ref(px * 4), got(px * 4);
         std::string cur;
         for (auto& v : vars) {
-            CK(hipMemset(out[2], 0xa5, px));
+            const size_t nb = v.group == "wide" ? px * 4 : px;  // fp32 output plane
+            CK(hipMemset(out[2], 0xa5, nb));
             v.launch(src(v, 1), out[2], c, 0);
             const hipError_t le = hipGetLastError();
             if (le != hipSuccess) {
@@ -211,13 +224,13 @@ int main(int argc, char** argv) {
             CK(hipDeviceSynchronize());
             if (v.group != cur) {
                 cur = v.group;
-                CK(hipMemcpy(ref.data(), out[2], px, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(ref.data(), out[2], nb, hipMemcpyDeviceToHost));
                 printf("check %-40s reference of group %s\n", v.name.c_str(), cur.c_str());
                 continue;
             }
             if (!v.check) continue;
-            CK(hipMemcpy(got.data(), out[2], px, hipMemcpyDeviceToHost));
-            const bool ok = memcmp(ref.data(), got.data(), px) == 0;
+            CK(hipMemcpy(got.data(), out[2], nb, hipMemcpyDeviceToHost));
+            const bool ok = memcmp(ref.data(), got.data(), nb) == 0;
             printf("check %-40s %s\n", v.name.c_str(), ok ? "bit-exact" : "MISMATCH");
             if (!ok) return 1;
         }
@@ -286,7 +299,7 @@ int main(int argc, char** argv) {
         if (t.empty()) continue;
         std::sort(t.begin(), t.end());
         const double med = t[t.size() / 2];
-        double bpp = vars[v].group == "inv" ? 5.0 : 2.0;
+        double bpp = vars[v].group == "inv" || vars[v].group == "wide" ? 5.0 : 2.0;
         if (vars[v].group == "rt") {
             const std::string& nm = vars[v].name;
             bpp = nm.find("(10 B") != std::string::npos  ? 10.0
