@@ -428,6 +428,27 @@ def test_fill_hash_matches_oracle(hp, oracle, dev, n, first):
     assert np.array_equal(to_host(buf), oracle.hash_u8(n, 42, first))
 
 
+@pytest.mark.parametrize("h,w", [(6560, 1280), (4376, 1920)])
+def test_video_widths_large_frames(hp, oracle, dev, h, w):
+    """Frames large enough for the one-lane-per-tile kernels under AUTO, at
+    widths that are not multiples of 512 px: 64-tile sets straddle two tile
+    rows (the kVarStraddle variant's two-run staged stores).  Forward to fp32
+    and int8, inverse from int8, and the one-pass round trip, all bit-exact."""
+    import torch
+    img = oracle.hash_u8(h * w, seed=17).reshape(h, w)
+    x = to_dev(img, dev)
+    q_ref = oracle.fdct(img)
+    r_ref = oracle.idct(q_ref)
+    q = hp.forward(x)
+    assert bits_equal(to_host(q), q_ref)
+    q8 = hp.forward(x, torch.empty((h, w), dtype=torch.int8, device=dev))
+    assert np.array_equal(to_host(q8), q_ref.astype(np.int8))
+    assert bits_equal(to_host(hp.inverse(q8)), r_ref)
+    coef, rec8, _ = hp.roundtrip(x, recon_dtype=torch.uint8, sums=False)
+    assert bits_equal(to_host(coef), q_ref)
+    assert np.array_equal(to_host(rec8), oracle.to_u8(r_ref))
+
+
 # --------------------------------------------------------------------- full-size configs
 def test_c2_1024_bitexact(hp, oracle, dev, golden):
     img = oracle.rand_u8(1024 * 1024).reshape(1024, 1024)

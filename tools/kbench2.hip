@@ -196,6 +196,9 @@ int main(int argc, char** argv) {
         {"rt", "rt fused u8 recon + sums, IEEE/fp32 q", rt_fused<kRtReconU8, true, false>, true},
         {"wide", "fwd u8->f32 tile (product)", f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"wide", "fwd u8->f32 tile panel 4096 px", f32_fwd<kProdVar<uint8_t, float> | F | kVarPanel>, true},
+        {"wide", "fwd u8->f32 tile nt loads", f32_fwd<kProdVar<uint8_t, float> | F | kVarNTLoad>, true},
+        {"wide", "fwd u8->f32 tile b256", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | F>, true},
+        {"wide", "fwd u8->f32 tile b1024", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | W1024 | F>, true},
         {"wide", "fwd u8->f32 tile (product) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | kVarNoStore>, false},
