@@ -237,8 +237,15 @@ def main():
             pass
 
 
-def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop, imgs, outs, px,
+def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop0, imgs, outs, px,
             n, extras):
+    def timed_loop(calls, steps, warmup):
+        # steady state: an untimed pass as long as the timed one first.  The
+        # VALU-heavy kernels run ~8 % slow for the first few ms after a change
+        # of load (memory-bound headline loop, or idle): a clock ramp, not the
+        # kernel (tools/seq_probe.py, profiles/r01/seq_probe.log)
+        return timed_loop0(calls, steps, max(warmup, steps))
+
     if True:
         steps = max(10, args.steps // 2)
         # fp32 in -> fp32 out (the reference's own data types; compat kernel)
