@@ -47,8 +47,13 @@ def main():
             f32 = [t.float() for t in ins]
             del ins
             outs = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in range(4)]
-            fw = us_per_launch([hpdct.bind("fwd", f32[s_], outs[s_], transform=T) for s_ in range(4)])
-            iv = us_per_launch([hpdct.bind("inv", outs[s_], f32[s_]) for s_ in range(4)])
+            # each measured after an untimed pass of the same loop (steady clocks: tools/seq_probe.py)
+            fcalls = [hpdct.bind("fwd", f32[s_], outs[s_], transform=T) for s_ in range(4)]
+            us_per_launch(fcalls)
+            fw = us_per_launch(fcalls)
+            icalls = [hpdct.bind("inv", outs[s_], f32[s_]) for s_ in range(4)]
+            us_per_launch(icalls)
+            iv = us_per_launch(icalls)
             px = h * w
             print(f"{h:6d} x {w:6d}  fwd f32 runtime-T {fw * 64 * 2**20 / px:8.2f}  inv f32 {iv * 64 * 2**20 / px:8.2f}"
                   "  us per 64 Mpx", flush=True)
