@@ -212,6 +212,22 @@ def test_forward_nonfinite_fp32_input(hp, oracle, dev):
     assert bits_equal(got, oracle.fdct(img, quant=False))
 
 
+@pytest.mark.parametrize("lo,hi", [(0.0, 255.0), (-700.0, 700.0), (-3000.0, 3000.0)])
+def test_fp32_input_quotient_range_check(hp, oracle, dev, lo, hi):
+    """fp32 input takes the verified 3-op quotient only for rows whose every
+    coefficient in the wave has |C| <= 4096 (duo kernel); these inputs give
+    all-in-range rows (pixel values), a mix, and mostly out-of-range rows.
+    Bit-exact either way, with the built-in and with the caller's T."""
+    import torch
+    img = np.random.default_rng(7).uniform(lo, hi, (256, 1024)).astype(np.float32)
+    if lo == 0.0:
+        img = np.round(img)
+    ref = oracle.fdct(img)
+    assert bits_equal(to_host(hp.forward(to_dev(img, dev))), ref)
+    T = torch.from_numpy(oracle.default_transform()).to(dev)
+    assert bits_equal(to_host(hp.forward(to_dev(img, dev), transform=T)), ref)
+
+
 def test_batch_of_frames(hp, oracle, dev):
     frames = np.random.default_rng(2).integers(0, 256, (3, 64, 128), dtype=np.uint8)
     got = to_host(hp.forward(to_dev(frames, dev)))
