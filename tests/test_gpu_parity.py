@@ -214,10 +214,11 @@ def test_forward_nonfinite_fp32_input(hp, oracle, dev):
 
 @pytest.mark.parametrize("lo,hi", [(0.0, 255.0), (-700.0, 700.0), (-3000.0, 3000.0)])
 def test_fp32_input_quotient_range_check(hp, oracle, dev, lo, hi):
-    """fp32 input takes the verified 3-op quotient only for rows whose every
-    coefficient in the wave has |C| <= 4096 (duo kernel); these inputs give
-    all-in-range rows (pixel values), a mix, and mostly out-of-range rows.
-    Bit-exact either way, with the built-in and with the caller's T."""
+    """fp32 input over three coefficient ranges: every |C| within the 3-op
+    quotient's verified |C| <= 4096 (pixel values), a mix, and mostly beyond
+    it (a range-checked fast quotient was measured for fp32 input and not
+    kept; fp32 input divides with IEEE division).
+    Bit-exact with the built-in and with the caller's T."""
     import torch
     img = np.random.default_rng(7).uniform(lo, hi, (256, 1024)).astype(np.float32)
     if lo == 0.0:
