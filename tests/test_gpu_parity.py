@@ -464,6 +464,11 @@ def test_video_widths_large_frames(hp, oracle, dev, h, w):
     coef, rec8, _ = hp.roundtrip(x, recon_dtype=torch.uint8, sums=False)
     assert bits_equal(to_host(coef), q_ref)
     assert np.array_equal(to_host(rec8), oracle.to_u8(r_ref))
+    # fp32 reconstruction: a second LDS-staged plane through the straddling sets
+    coef, recf, sums = hp.roundtrip(x, recon_dtype=torch.float32, sums=True)
+    assert bits_equal(to_host(coef), q_ref)
+    assert bits_equal(to_host(recf), r_ref)
+    assert sums["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
 
 
 # --------------------------------------------------------------------- full-size configs
