@@ -6,6 +6,11 @@ achieved fraction of the MI355X HBM roofline, at 1/2/4/8 GPUs.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) the parent process does
+not import torch or touch the GPU: it starts N child processes of this script
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set),
+waits for all of them and exits non-zero if any fails.
+
 A step = one launch of the fused gfx950 forward kernel over one 8192x8192
 frame already resident in HBM (uint8 pixels in, fp32 quantised coefficients
 out, reference layout; 5 algorithmic bytes per pixel).  Frames rotate over
@@ -24,6 +29,8 @@ every timed number is the HIP kernel.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,6 +43,8 @@ METRIC = "Gpixel/s fwd-DCT (8192×8192) + achieved HBM % at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 T4_FWD_8192_MS = 14.70         # README.md:55, T4
 BYTES_PER_PX = {"u8_f32": 5, "f32_f32": 8, "u8_i8": 2, "inv_f32_f32": 8}
+EXTRA_STEPS = 100              # timed launches per extra (independent of --steps)
+EXTRA_WARM_S = 0.02            # untimed steady-state lead-in per extra (>= 20 ms)
 
 
 def parse():
@@ -58,17 +67,56 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """One child process per rank (no torch, no HIP in this parent), the
+    torch.distributed env contract set for each; returns the first non-zero
+    child exit code (the others are then terminated), else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # a peer is gone: the others would block in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("--gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
     import hpdct
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     # one process per GPU: LOCAL_RANK is the device (modulo the visible devices,
     # so a gloo rehearsal can put several ranks on one GPU)
     ndev = torch.cuda.device_count()
@@ -223,6 +271,13 @@ def main():
         except Exception as e:  # report, keep the headline line
             extras["error"] = f"{type(e).__name__}: {e}"[:500]
         result["extras"] = extras
+        c4 = extras.get("c4", {})
+        # the north_star row-shard figures (C4, 16384^2 over the ranks), top level
+        for key in ("compute_speedup_vs_1gpu", "gather_ms", "gather_int8_ms", "sharded_equals_unsharded"):
+            if key in c4:
+                result["c4_" + key] = c4[key]
+        if "compute_ms_max_rank" in c4:
+            result["c4_compute_ms_max_rank"] = c4["compute_ms_max_rank"]
 
     # ------------------------------------------------------------ CPU baseline
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -235,19 +290,35 @@ def main():
             dist.destroy_process_group()
         except Exception:
             pass
+    return 0
 
 
 def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop0, imgs, outs, px,
             n, extras):
     def timed_loop(calls, steps, warmup):
-        # steady state: an untimed pass as long as the timed one first.  The
-        # VALU-heavy kernels run ~8 % slow for the first few ms after a change
-        # of load (memory-bound headline loop, or idle): a clock ramp, not the
-        # kernel (tools/seq_probe.py, profiles/r01/seq_probe.log)
-        return timed_loop0(calls, steps, max(warmup, steps))
+        """Steady state, independent of --steps: untimed launches for at least
+        max(20 ms, the timed region's expected length), then `steps` (>= 100
+        for the short kernels) timed launches.  The VALU-heavy kernels run
+        ~8 % slow for the first few ms after a change of load (memory-bound
+        headline loop, or idle): a clock ramp, not the kernel
+        (tools/seq_probe.py, profiles/r01/seq_probe.log)."""
+        k = len(calls)
+        t0 = time.perf_counter()
+        for i in range(max(warmup, 2 * k)):
+            calls[i % k]()
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t0) / max(warmup, 2 * k)
+        target = max(EXTRA_WARM_S, per * steps)
+        i, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < target:
+            for _ in range(8):
+                calls[i % k]()
+                i += 1
+            torch.cuda.synchronize()
+        return timed_loop0(calls, steps, 0)
 
     if True:
-        steps = max(10, args.steps // 2)
+        steps = EXTRA_STEPS
         # fp32 in -> fp32 out (the reference's own data types; compat kernel)
         f32_in = [imgs[s].float() for s in range(args.sets)]
         f32_out = outs[:len(f32_in)]
@@ -275,7 +346,7 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         bres = torch.empty_like(bimg)
         for kind in ("reference_3pass", "fastappr_3pass"):
             calls = [lambda k=kind: hpdct.baseline_forward(k, bimg, btmp, bres, T, stream=stream)]
-            bsteps = max(10, steps // 4)
+            bsteps = 40
             rms, k, _ = timed_loop(calls, bsteps, 3)
             extras["baseline_" + kind] = {
                 "ms_per_frame": round(rms / bsteps, 4), "gpx_s": round(px / (rms / bsteps * 1e-3) / 1e9, 2),
@@ -349,7 +420,8 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         del c2b_in, c2b_out
         torch.cuda.empty_cache()
         if not args.no_c4c5:
-            extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks)
+            extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks,
+                               timed_loop)
             extras["c5"] = _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks)
 
 
@@ -410,7 +482,26 @@ def _line(px, ms_step, kern_ms, bpp, world, pmc_key=None, n=None):
     return out
 
 
-def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks):
+def _steady_ms(torch, calls, steps, stream):
+    """Rank-local steady-state timing (no barrier): >= 20 ms of untimed
+    launches, then `steps` launches between two events on `stream`."""
+    i, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < EXTRA_WARM_S or i < 2 * len(calls):
+        calls[i % len(calls)]()
+        i += 1
+        if i % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for i in range(steps):
+        calls[i % len(calls)]()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop):
     """C4: one 16384^2 frame row-sharded over the ranks (device-generated by
     the stateless hash so no H2D), forward kernel per slab, then the RCCL
     gather of the fp32 coefficient slabs to rank 0, timed separately."""
@@ -425,21 +516,14 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     ys = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(2)]
     x, y = xs[0], ys[0]
     calls = [hpdct.bind("fwd", xs[i], ys[i], stream=stream) for i in range(2)]
-    for i in range(4):
-        calls[i % 2]()
-    reps = 20
-    torch.cuda.synchronize()
-    barrier()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(stream)
-    for i in range(reps):
-        calls[i % 2]()
-    b.record(stream)
-    torch.cuda.synchronize()
-    compute_ms = max_over_ranks(a.elapsed_time(b) / reps)
+    reps = EXTRA_STEPS
+    rms, _, _ = timed_loop(calls, reps, 4)
+    compute_ms = max_over_ranks(rms / reps)
     out = {"frame": [n, n], "rows_per_rank": rows, "compute_ms_max_rank": round(compute_ms, 4),
-           "compute_gpx_s": round(n * n / (compute_ms * 1e-3) / 1e9, 2)}
+           "compute_gpx_s": round(n * n / (compute_ms * 1e-3) / 1e9, 2),
+           "compute_hbm_frac_max_rank": round(5 * rows * n / (compute_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if world > 1:
+        hpdct.forward(x, y)  # y = this rank's slab of the frame (set 0)
         gather_ms = []
         full = None
         for _ in range(3):
@@ -481,18 +565,11 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
             xf2 = xf.clone()
             ref2 = torch.empty_like(ref)
             fcalls = [hpdct.bind("fwd", xf, ref, stream=stream), hpdct.bind("fwd", xf2, ref2, stream=stream)]
-            for i in range(4):
-                fcalls[i % 2]()
-            fa, fb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            fa.record(stream)
-            for i in range(reps):
-                fcalls[i % 2]()
-            fb.record(stream)
-            torch.cuda.synchronize()
-            one_gpu_ms = fa.elapsed_time(fb) / reps
+            one_gpu_ms = _steady_ms(torch, fcalls, reps, stream)
             out["one_gpu_full_frame_ms"] = round(one_gpu_ms, 4)
             out["compute_speedup_vs_1gpu"] = round(one_gpu_ms / compute_ms, 2)
             del xf, ref, xf2, ref2
+        barrier()
     del x, y, xs, ys
     torch.cuda.empty_cache()
     return out
@@ -568,4 +645,4 @@ def _cpu_baseline(n):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

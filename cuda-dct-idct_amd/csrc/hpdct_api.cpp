@@ -66,6 +66,15 @@ hpdct_status fail(hpdct_status st, const std::string& msg) {
     return st;
 }
 
+}  // namespace
+
+int hpdct::set_last_error(int st, const char* msg) {
+    g_last_error = msg ? msg : "";
+    return st;
+}
+
+namespace {
+
 hpdct_status device_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return HPDCT_SUCCESS;
     return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));

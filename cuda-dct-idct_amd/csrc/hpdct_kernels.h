@@ -63,4 +63,8 @@ hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t fi
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.
 int mapping_mode();
 
+// Records msg as hpdct_last_error_string() of this thread and returns st
+// (hpdct_api.cpp; every C-ABI error return goes through it).
+int set_last_error(int st, const char* msg);
+
 }  // namespace hpdct

@@ -68,7 +68,13 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
                                                                           QParams qp) {
     constexpr unsigned kVar =
         (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) | (kStraddle ? kVarStraddle : 0u);
-    const TSource<true, true> T(nullptr);  // built-in T; u8 pixels and int8-range q are finite
+    // built-in T.  The forward's u8 pixels are finite, so the zero terms of T
+    // are skipped exactly; so are the inverse's for kFast (int8-range q times
+    // Q in 1..255).  With IEEE division and a caller's table, q = round(C/Q)
+    // may be +-inf (|Q| tiny): then the inverse runs the full chain, where
+    // 0 * inf = NaN as in the reference and the standalone fp32 inverse.
+    const TSource<true, true> T(nullptr);
+    const TSource<true, false> T_full(nullptr);
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, float> coef_sink{coef, g.width, slots};
     const RowSink<kVar, float> rf32_sink{static_cast<float*>(recon), g.width, slots};
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
                 d[i][j] = qv * qp.q.v[i * 8 + j];
             });
         });
-        idct_tile(T, d, [&](auto v, float (&r)[8]) {
+        auto emit_inv = [&](auto v, float (&r)[8]) {
             unroll<8>([&](auto u) { r[u] = r[u] + 128.0f; });
             uint2 r8;  // convertToUnsignedChar (utils.cu:21): clamp, truncate, packed
             if constexpr (kStats || kRecon == kRtReconU8) {
@@ -155,13 +161,22 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
             } else if constexpr (kRecon == kRtReconF32) {
                 rf32_sink(v, p, ok, seg, r);
             }
-        });
+        };
+        if constexpr (kFast) {
+            idct_tile(T, d, emit_inv);
+        } else if (wave_tame(d)) {
+            idct_tile(T, d, emit_inv);
+        } else {
+            idct_tile(T_full, d, emit_inv);
+        }
     });
 
     if constexpr (kStats) {
         // lanes without a tile (ragged last set, or waves past the end) hold zeros
-        unsigned long long f = static_cast<unsigned long long>(
-            __builtin_rintf(acc_f * kRtFixScale));  // < 2^24 * 2^16: exact in the convert
+        // < 2^24 * 2^16 for any finite reconstruction: exact in the convert; a
+        // non-finite one (IEEE path, extreme table) saturates the field
+        const float fx = __builtin_rintf(acc_f * kRtFixScale);
+        unsigned long long f = fx < 1.8e19f ? static_cast<unsigned long long>(fx) : ~0ull >> 8;
         unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
         unsigned long long xx = static_cast<unsigned long long>(acc_xx);
         f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);

@@ -16,8 +16,16 @@
 #include <vector>
 
 #include "hpdct.h"
+#include "hpdct_kernels.h"
 
 namespace {
+hpdct_status fail(hpdct_status st, const std::string& msg) {
+    return static_cast<hpdct_status>(hpdct::set_last_error(st, msg.c_str()));
+}
+hpdct_status device_fail(hipError_t e, const char* what) {
+    return fail(HPDCT_ERROR_DEVICE, std::string("hpdct_stream_forward: ") + what + ": " + hipGetErrorString(e));
+}
+
 struct DeviceRing {
     std::vector<hipStream_t> streams;
     std::vector<void*> in, out;
@@ -32,11 +40,18 @@ struct DeviceRing {
 extern "C" hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
                                              int64_t height, int64_t width, hpdct_dtype out_type, int nstreams,
                                              float* elapsed_ms) {
-    if (!h_frames || !h_coef || n_frames < 0 || nstreams < 1 || nstreams > 16) return HPDCT_ERROR_INVALID_VALUE;
-    if (out_type != HPDCT_F32 && out_type != HPDCT_I8) return HPDCT_ERROR_UNSUPPORTED;
-    if (height <= 0 || width <= 0 || height % 8 || width % 8) return HPDCT_ERROR_INVALID_VALUE;
+    if (!h_frames || !h_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: null frame list");
+    if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: negative frame count");
+    if (nstreams < 1 || nstreams > 16)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: nstreams must be in 1..16");
+    if (out_type != HPDCT_F32 && out_type != HPDCT_I8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "hpdct_stream_forward: output must be HPDCT_F32 or HPDCT_I8");
+    if (height <= 0 || width <= 0 || height % 8 || width % 8)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: height and width must be positive multiples of 8");
     for (int64_t f = 0; f < n_frames; ++f)
-        if (!h_frames[f] || !h_coef[f]) return HPDCT_ERROR_INVALID_VALUE;
+        if (!h_frames[f] || !h_coef[f])
+            return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: null frame or output pointer at index " +
+                                                       std::to_string(f));
     if (n_frames == 0) {
         if (elapsed_ms) *elapsed_ms = 0.0f;
         return HPDCT_SUCCESS;
@@ -47,15 +62,20 @@ extern "C" hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, voi
     for (int s = 0; s < nstreams; ++s) {
         hipStream_t st;
         void *di = nullptr, *dout = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return HPDCT_ERROR_DEVICE;
+        hipError_t he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (he != hipSuccess) return device_fail(he, "hipStreamCreateWithFlags");
         ring.streams.push_back(st);
-        if (hipMalloc(&di, px) != hipSuccess) return HPDCT_ERROR_DEVICE;
+        if ((he = hipMalloc(&di, px)) != hipSuccess) return device_fail(he, "hipMalloc (frames)");
         ring.in.push_back(di);
-        if (hipMalloc(&dout, out_bytes) != hipSuccess) return HPDCT_ERROR_DEVICE;
+        if ((he = hipMalloc(&dout, out_bytes)) != hipSuccess) return device_fail(he, "hipMalloc (coefficients)");
         ring.out.push_back(dout);
     }
     hipEvent_t t0, t1;
-    if (hipEventCreate(&t0) != hipSuccess || hipEventCreate(&t1) != hipSuccess) return HPDCT_ERROR_DEVICE;
+    if (hipError_t he = hipEventCreate(&t0); he != hipSuccess) return device_fail(he, "hipEventCreate");
+    if (hipError_t he = hipEventCreate(&t1); he != hipSuccess) {
+        (void)hipEventDestroy(t0);
+        return device_fail(he, "hipEventCreate");
+    }
     // start marker: every stream waits for it, so the timed region holds the whole batch
     hipError_t e = hipEventRecord(t0, ring.streams[0]);
     for (int s = 1; s < nstreams && e == hipSuccess; ++s) e = hipStreamWaitEvent(ring.streams[s], t0, 0);
@@ -90,7 +110,7 @@ extern "C" hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, voi
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     for (hipStream_t st : ring.streams) (void)hipStreamSynchronize(st);
-    if (e != hipSuccess) return HPDCT_ERROR_DEVICE;
+    if (e != hipSuccess) return device_fail(e, "copy/compute pipeline");
     if (elapsed_ms) *elapsed_ms = ms;
     return HPDCT_SUCCESS;
 }

@@ -223,9 +223,52 @@ def _hw(t, height, width):
     if height is None or width is None:
         if t.dim() < 2:
             raise HpdctError(1, "pass height/width for a flat tensor")
-        height = t.numel() // t.shape[-1]
+        height = t.numel() // t.shape[-1] if t.shape[-1] else 0
         width = t.shape[-1]
-    return int(height), int(width)
+    h, w = int(height), int(width)
+    if h < 0 or w < 0:
+        raise HpdctError(1, f"negative frame shape {h}x{w}")
+    if h * w > t.numel():
+        raise HpdctError(1, f"a {h}x{w} frame needs {h * w} elements, the source holds {t.numel()}")
+    return h, w
+
+
+def _device_plane(t, what: str, device, need: int, dtypes=None):
+    """The C-ABI cannot see buffer sizes: every device plane is checked here
+    (CUDA, contiguous, on `device`, >= `need` elements, dtype allowed)."""
+    if not hasattr(t, "is_cuda") or not t.is_cuda:
+        raise HpdctError(1, f"{what} must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise HpdctError(1, f"{what} must be contiguous")
+    if device is not None and t.device != device:
+        raise HpdctError(1, f"{what} is on {t.device}, the source on {device}")
+    if t.numel() < need:
+        raise HpdctError(1, f"{what} holds {t.numel()} elements, {need} needed")
+    if dtypes is not None and t.dtype not in dtypes:
+        raise HpdctError(2, f"{what} dtype {t.dtype} not in {list(dtypes)}")
+
+
+def _transform_ptr(transform, device):
+    """None (built-in T) or a contiguous 64-element float32 CUDA tensor."""
+    if transform is None:
+        return None
+    torch = _torch()
+    _device_plane(transform, "transform", device, 64, (torch.float32,))
+    if transform.numel() != 64:
+        raise HpdctError(1, f"transform must hold 64 floats, not {transform.numel()}")
+    return ctypes.c_void_p(transform.data_ptr())
+
+
+def _planes(src, dst, direction: str, height, width):
+    """Shape and buffer checks of one forward/inverse launch; returns (h, w)."""
+    torch = _torch()
+    what = "image" if direction == "fwd" else "coefficients"
+    ins = (torch.uint8, torch.float32) if direction == "fwd" else (torch.int8, torch.float32)
+    outs = (torch.float32, torch.int8) if direction == "fwd" else (torch.float32, torch.uint8)
+    _device_plane(src, what, None, 0, ins)
+    h, w = _hw(src, height, width)
+    _device_plane(dst, "out", src.device, h * w, outs)
+    return h, w
 
 
 def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, writeback_shift=False,
@@ -236,14 +279,13 @@ def forward(image, out=None, *, out_dtype=None, transform=None, quantise=True, w
     frames is treated as one (F*H) x W image).  Returns the coefficient
     tensor (float32 by default, int8 on request) in the reference layout."""
     torch = _torch()
-    if not image.is_cuda or not image.is_contiguous():
-        raise HpdctError(1, "image must be a contiguous CUDA tensor")
-    h, w = _hw(image, height, width)
+    _device_plane(image, "image", None, 0)
     if out is None:
         out = torch.empty(image.shape, dtype=out_dtype or torch.float32, device=image.device)
+    h, w = _planes(image, out, "fwd", height, width)
     flags = (0 if quantise else FLAG_NO_QUANT) | (FLAG_WRITEBACK_SHIFT if writeback_shift else 0) | \
         (0 if level_shift else FLAG_NO_SHIFT) | (FLAG_ROW_FIRST if row_first else 0)
-    tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
+    tptr = _transform_ptr(transform, image.device)
     _check(load_library().hpdct_forward(ctypes.c_void_p(image.data_ptr()), _dtype_code(image),
                                         ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
                                         flags, _stream_ptr(stream)))
@@ -255,14 +297,13 @@ def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, 
     """Fused inverse pass: T^T.(q*Q).T + 128 per tile.  out float32 (no clamp,
     as the reference) or uint8 (clamp + truncate, convertToUnsignedChar)."""
     torch = _torch()
-    if not coef.is_cuda or not coef.is_contiguous():
-        raise HpdctError(1, "coefficients must be a contiguous CUDA tensor")
-    h, w = _hw(coef, height, width)
+    _device_plane(coef, "coefficients", None, 0)
     if out is None:
         out = torch.empty(coef.shape, dtype=out_dtype or torch.float32, device=coef.device)
+    h, w = _planes(coef, out, "inv", height, width)
     flags = (0 if dequantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT) | \
         (FLAG_ROW_FIRST if row_first else 0) | (FLAG_WRITEBACK_DEQUANT if writeback_dequant else 0)
-    tptr = None if transform is None else ctypes.c_void_p(transform.data_ptr())
+    tptr = _transform_ptr(transform, coef.device)
     _check(load_library().hpdct_inverse(ctypes.c_void_p(coef.data_ptr()), _dtype_code(coef),
                                         ctypes.c_void_p(out.data_ptr()), _dtype_code(out), h, w, tptr,
                                         flags, _stream_ptr(stream)))
@@ -274,15 +315,15 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
     """Pre-resolve every argument of one forward ("fwd") or inverse ("inv")
     launch and return a zero-argument callable: the per-call host cost is one
     ctypes call (used by bench.py's timed loop)."""
-    if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()):
-        raise HpdctError(1, "src/dst must be contiguous CUDA tensors")
-    h, w = _hw(src, height, width)
+    if direction not in ("fwd", "inv"):
+        raise ValueError('direction must be "fwd" or "inv"')
+    h, w = _planes(src, dst, direction, height, width)
     lib = load_library()
     fn = {"fwd": lib.hpdct_forward, "inv": lib.hpdct_inverse}[direction]
     flags = (0 if quantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT) | \
         (FLAG_WRITEBACK_SHIFT if writeback_shift else 0)
     args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(dst.data_ptr()), _dtype_code(dst),
-            h, w, None if transform is None else ctypes.c_void_p(transform.data_ptr()), flags, _stream_ptr(stream))
+            h, w, _transform_ptr(transform, src.device), flags, _stream_ptr(stream))
 
     def call():
         st = fn(*args)
@@ -295,12 +336,14 @@ SSE_F32_UNIT = 1.0 / 65536.0  # HPDCT_SSE_F32_UNIT
 
 
 def _roundtrip_args(image, coef, recon, sums_buf, height, width, stream):
-    for t in (image, coef) + ((recon,) if recon is not None else ()):
-        if not t.is_cuda or not t.is_contiguous():
-            raise HpdctError(1, "image, coefficients and reconstruction must be contiguous CUDA tensors")
-    if _dtype_code(image) != U8 or _dtype_code(coef) != F32:
-        raise HpdctError(2, "round trip: uint8 image -> float32 coefficients")
+    torch = _torch()
+    _device_plane(image, "image", None, 0, (torch.uint8,))
     h, w = _hw(image, height, width)
+    _device_plane(coef, "coefficients", image.device, h * w, (torch.float32,))
+    if recon is not None:
+        _device_plane(recon, "reconstruction", image.device, h * w, (torch.uint8, torch.float32))
+    if sums_buf is not None:
+        _device_plane(sums_buf, "sums buffer", image.device, 3, (torch.int64,))
     return (ctypes.c_void_p(image.data_ptr()), ctypes.c_void_p(coef.data_ptr()),
             None if recon is None else ctypes.c_void_p(recon.data_ptr()),
             F32 if recon is None else _dtype_code(recon),
@@ -357,7 +400,15 @@ def baseline_forward(kind: str, image, tmp, result, transform, stream=None) -> N
     """A/B baselines (include/hpdct_baseline.h): the reference's 3-launch
     HpApprDCT structure or the fastApprDCT row-per-thread structure on the GPU.
     Mutates `image` to X-128 like the reference."""
+    if kind not in BASELINES:
+        raise ValueError(f"kind must be one of {sorted(BASELINES)}")
+    torch = _torch()
+    _device_plane(image, "image", None, 0, (torch.float32,))
     h, w = _hw(image, None, None)
+    for t, what in ((tmp, "tmp"), (result, "result")):
+        _device_plane(t, what, image.device, h * w, (torch.float32,))
+    if _transform_ptr(transform, image.device) is None:
+        raise HpdctError(1, "the baselines take the caller's transform (64 floats on the device)")
     st = load_library().hpdct_baseline_forward(BASELINES[kind], ctypes.c_void_p(image.data_ptr()),
                                                ctypes.c_void_p(tmp.data_ptr()), ctypes.c_void_p(result.data_ptr()),
                                                h, w, ctypes.c_void_p(transform.data_ptr()), _stream_ptr(stream))
@@ -370,10 +421,25 @@ def stream_forward(frames, outs, nstreams: int = 3) -> float:
     with H2D / kernel / D2H overlapped over `nstreams` HIP streams.  `frames`
     and `outs` are equal-length lists of CPU tensors (entries may repeat).
     Returns the device-timed milliseconds of the whole batch."""
+    torch = _torch()
     n = len(frames)
     if n != len(outs) or n == 0:
         raise HpdctError(1, "frames and outs must be non-empty lists of equal length")
     h, w = _hw(frames[0], None, None)
+    # the library copies h*w bytes in and h*w coefficients out per frame from
+    # these host pointers: every entry must be exactly that large
+    shape, odt = tuple(frames[0].shape), outs[0].dtype
+    if odt not in (torch.float32, torch.int8):
+        raise HpdctError(2, f"coefficient planes must be float32 or int8, not {odt}")
+    for i, (f, o) in enumerate(zip(frames, outs)):
+        if f.is_cuda or o.is_cuda:
+            raise HpdctError(1, f"frame {i}: frames and outs are host (pinned) tensors")
+        if not (f.is_contiguous() and o.is_contiguous()):
+            raise HpdctError(1, f"frame {i}: host tensors must be contiguous")
+        if f.dtype != torch.uint8 or tuple(f.shape) != shape:
+            raise HpdctError(1, f"frame {i}: expected a uint8 {shape} frame, got {f.dtype} {tuple(f.shape)}")
+        if o.dtype != odt or o.numel() != h * w:
+            raise HpdctError(1, f"out {i}: expected {h * w} {odt} elements, got {o.numel()} {o.dtype}")
     fp = (ctypes.c_void_p * n)(*[f.data_ptr() for f in frames])
     op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
     ms = ctypes.c_float()
@@ -384,6 +450,7 @@ def stream_forward(frames, outs, nstreams: int = 3) -> float:
 
 def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):
     """Device-side synthetic frame: out[i] = splitmix64(seed, first_index+i) & 255."""
+    _device_plane(out, "out", None, 0, (_torch().uint8,))
     _check(load_library().hpdct_fill_hash_u8(ctypes.c_void_p(out.data_ptr()), out.numel(),
                                              ctypes.c_uint64(seed), first_index, _stream_ptr(stream)))
     return out
@@ -392,34 +459,43 @@ def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):
 # ---------------------------------------------------------------------------
 # the reference's own C++ entry points (compat layer, synchronous, prints)
 # ---------------------------------------------------------------------------
+def _compat_call(key, image_matrix, img_height, img_width, transform_matrix, result, *extra):
+    """Buffer checks the C++ entry points cannot make (they see raw pointers):
+    fp32 CUDA planes of >= h*w elements and a 64-float device T.  Shape
+    errors the reference itself reports (W, H not multiples of 8) are left to
+    the library, which prints and exits like CHECK_CUDA."""
+    torch = _torch()
+    h, w = int(img_height), int(img_width)
+    need = max(h, 0) * max(w, 0)
+    _device_plane(image_matrix, "image_matrix", None, need, (torch.float32,))
+    _device_plane(result, "result", image_matrix.device, need, (torch.float32,))
+    tptr = _transform_ptr(transform_matrix, image_matrix.device)
+    if tptr is None:
+        raise HpdctError(1, "transform_matrix: the reference entry points take the caller's device T")
+    f = getattr(load_library(), COMPAT_SYMBOLS[key])
+    f(ctypes.c_void_p(image_matrix.data_ptr()), h, w, tptr, ctypes.c_void_p(result.data_ptr()), *extra)
+
+
 def dct_all_blocks_cuda(image_matrix, img_height: int, img_width: int, transform_matrix, result) -> None:
     """main_newAppr.cu:252-291 semantics: device fp32 buffers, caller's T,
     X-128 left in image_matrix, timing line on stdout, exits on error."""
-    f = getattr(load_library(), COMPAT_SYMBOLS["dct_all_blocks_cuda"])
-    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
-      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()))
+    _compat_call("dct_all_blocks_cuda", image_matrix, img_height, img_width, transform_matrix, result)
 
 
 def idct_all_blocks_cuda(image_matrix, img_height: int, img_width: int, transform_matrix, result) -> None:
     """main_newAppr.cu:293-332 semantics."""
-    f = getattr(load_library(), COMPAT_SYMBOLS["idct_all_blocks_cuda"])
-    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
-      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()))
+    _compat_call("idct_all_blocks_cuda", image_matrix, img_height, img_width, transform_matrix, result)
 
 
 def dct_all_blocks(image_matrix, img_height: int, img_width: int, transform_matrix, result, handle=None) -> None:
     """cublasDCTv2 surface (main_cublass_2.cu:197-252): row pass first, X-128
     left in image_matrix; the cuBLAS handle is accepted and ignored."""
-    f = getattr(load_library(), COMPAT_SYMBOLS["dct_all_blocks"])
-    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
-      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()), handle)
+    _compat_call("dct_all_blocks", image_matrix, img_height, img_width, transform_matrix, result, handle)
 
 
 def idct_all_blocks(image_matrix, img_height: int, img_width: int, transform_matrix, result, handle=None) -> None:
     """main_cublass_2.cu:257-311: q*Q left in image_matrix, D.T first."""
-    f = getattr(load_library(), COMPAT_SYMBOLS["idct_all_blocks"])
-    f(ctypes.c_void_p(image_matrix.data_ptr()), int(img_height), int(img_width),
-      ctypes.c_void_p(transform_matrix.data_ptr()), ctypes.c_void_p(result.data_ptr()), handle)
+    _compat_call("idct_all_blocks", image_matrix, img_height, img_width, transform_matrix, result, handle)
 
 
 # ---------------------------------------------------------------------------

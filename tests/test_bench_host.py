@@ -38,3 +38,68 @@ def test_defaults_are_the_driver_contract(monkeypatch):
     assert args.gpus == 1 and args.size == 8192 and args.sets >= 3
     assert args.steps > 0 and args.warmup > 0 and args.backend == "nccl"
     assert bench.BYTES_PER_PX["u8_f32"] == 5 and bench.HBM_PEAK_GBS == 8000.0
+
+
+def test_gpus_n_self_launches_ranks_without_torch(tmp_path):
+    """`python bench.py --gpus 2` with no launcher: the parent starts 2 child
+    processes with the torch.distributed env contract and never imports torch
+    (no HIP in the parent: the children own the GPUs)."""
+    import subprocess
+    script = tmp_path / "probe.py"
+    script.write_text(f"""
+import json, sys
+sys.path.insert(0, {ROOT!r})
+import bench
+seen = []
+class FakeProc:
+    def __init__(self, cmd, env):
+        seen.append({{k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}})
+        self.cmd = cmd
+    def poll(self):
+        return 0
+    def terminate(self):
+        pass
+bench.subprocess.Popen = FakeProc
+sys.argv = ["bench.py", "--gpus", "2", "--steps", "3"]
+rc = bench.main()
+print(json.dumps({{"rc": rc, "seen": seen, "torch": "torch" in sys.modules}}))
+""")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120)
+    import json
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["rc"] == 0 and res["torch"] is False
+    assert [s["RANK"] for s in res["seen"]] == ["0", "1"]
+    assert all(s["WORLD_SIZE"] == "2" and s["MASTER_ADDR"] == "127.0.0.1" for s in res["seen"])
+    assert len({s["MASTER_PORT"] for s in res["seen"]}) == 1
+
+
+def test_gpus_n_fails_when_a_rank_fails(tmp_path):
+    """A failing child makes the parent exit non-zero (and stops its peers)."""
+    import subprocess
+    script = tmp_path / "probe.py"
+    script.write_text(f"""
+import sys
+sys.path.insert(0, {ROOT!r})
+import bench
+class FakeProc:
+    n = 0
+    def __init__(self, cmd, env):
+        self.rank = int(env["RANK"]); self.killed = False
+    def poll(self):
+        return 3 if self.rank == 1 else (-15 if self.killed else None)
+    def terminate(self):
+        self.killed = True
+bench.subprocess.Popen = FakeProc
+sys.argv = ["bench.py", "--gpus", "4"]
+sys.exit(bench.main())
+""")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3
+
+
+def test_world_size_mismatch_is_an_error(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    assert bench.main() == 2

@@ -153,6 +153,47 @@ def test_roundtrip_quant_tables(hp, oracle, dev, qtab):
     check_sums(got, sums)
 
 
+def nan_aware_bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(np.where(na, 0, a.view(np.uint32)),
+                                                     np.where(nb, 0, b.view(np.uint32)))
+
+
+@pytest.mark.parametrize("tiny", [1e-40, -1e-40, 1e-38])
+def test_roundtrip_extreme_quant_table(hp, oracle, dev, tiny):
+    """A subnormal / tiny entry of a caller's table (accepted: finite and
+    non-zero) makes round(C/Q) infinite under IEEE division; the reference's
+    inverse then multiplies those infinities by the zero entries of T and gets
+    NaN (0 * inf).  The one-pass round trip must agree with the oracle and
+    with forward + standalone inverse: full chain for such waves.  The integer
+    sums stay exact (the uint8 reconstruction clamps NaN to 0)."""
+    import torch
+    rng = np.random.default_rng(99)
+    Q = rng.uniform(1.0, 40.0, (8, 8)).astype(np.float32)
+    Q[0, 2] = np.float32(tiny)
+    Q[3, 1] = np.float32(tiny)
+    img = rng.integers(0, 256, (64, 4096), dtype=np.uint8)
+    img[:, 512:] = 128  # tiles with C == 0: 0 / tiny = 0 stays finite there
+    q, r, r8, sums = expected(oracle, img, Q=Q)
+    assert np.isinf(q).any() and np.isnan(r).any()
+    hp.set_quant_table(Q)
+    try:
+        x = to_dev(img, dev)
+        coef, rec8, got = hp.roundtrip(x, recon_dtype=torch.uint8, sums=True)
+        _, recf, _ = hp.roundtrip(x, recon_dtype=torch.float32)
+        two = hp.inverse(hp.forward(x))
+        torch.cuda.synchronize()
+    finally:
+        hp.set_quant_table(None)
+    assert bits_equal(to_host(coef), q)
+    assert np.array_equal(to_host(rec8), r8)
+    assert nan_aware_bits_equal(to_host(recf), r)
+    assert nan_aware_bits_equal(to_host(two), r)
+    assert got["sum_x2"] == sums["sum_x2"] and got["sse_u8"] == sums["sse_u8"]
+
+
 def test_roundtrip_extremes(hp, oracle, dev):
     """All-0 / all-255 / sign-pattern tiles: the largest |q| and the most
     clamping in the uint8 reconstruction."""
