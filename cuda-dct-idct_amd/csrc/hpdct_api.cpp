@@ -15,6 +15,7 @@
 
 #include "hpdct.h"
 #include "hpdct_kernels.h"
+#include "hpdct_tables.h"
 
 #define HPDCT_VERSION_STRING "hpdct 0.1.0 (gfx950)"
 
@@ -24,26 +25,10 @@ using hpdct::Mat64;
 using hpdct::QParams;
 using hpdct::TileGrid;
 
-// JPEG luminance table and the HpApprDCT matrix (main_newAppr.cu:60-81),
-// host copies; the device copies are compile-time constants in hpdct_tile.hpp.
-constexpr float kDefaultQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
-                                 14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
-                                 18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
-                                 49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
-#define TA ((float)0.35355339)
-#define TH ((float)0.5)
-#define TB ((float)0.4472136)
-#define TC ((float)0.2236068)
-#define TD ((float)0.70710678)
-constexpr float kDefaultT[64] = {TA, TA,  TA,  TA,  TA,  TA,  TA,  TA,  TH, TH,  0,   0,   0,   0,   -TH, -TH,
-                                 TB, TC,  -TC, -TB, -TB, -TC, TC,  TB,  0,  0,   -TD, 0,   0,   TD,  0,   0,
-                                 TA, -TA, -TA, TA,  TA,  -TA, -TA, TA,  TH, -TH, 0,   0,   0,   0,   TH,  -TH,
-                                 TC, -TB, TB,  -TC, -TC, TB,  -TB, TC,  0,  0,   0,   -TD, TD,  0,   0,   0};
-#undef TA
-#undef TH
-#undef TB
-#undef TC
-#undef TD
+// JPEG luminance table and the HpApprDCT matrix (main_newAppr.cu:60-81): the
+// same constexpr arrays the kernels compile into immediates (hpdct_tables.h).
+constexpr const float (&kDefaultQ)[64] = hpdct::tables::kQ;
+constexpr const float (&kDefaultT)[64] = hpdct::tables::kT;
 
 // hpdct_mapping in force: -1 = not yet read from HPDCT_MAPPING.
 std::atomic<int> g_mapping{-1};

@@ -29,38 +29,22 @@
 #include <utility>
 
 #include "hpdct_kernels.h"
+#include "hpdct_tables.h"
 
 namespace hpdct {
 
 // ---------------------------------------------------------------------------
-// Tables.  The reference stores double literals into a float array
-// (main_newAppr.cu:73-81), so each entry is (float)(double)literal.
+// Tables: the built-in T (its entries become instruction immediates) and the
+// default Q, both from the one shared copy in hpdct_tables.h
+// (main_newAppr.cu:60-81, pinned to the reference's text by the tests).
 // ---------------------------------------------------------------------------
-#define HPDCT_TA ((float)0.35355339)
-#define HPDCT_TH ((float)0.5)
-#define HPDCT_TB ((float)0.4472136)
-#define HPDCT_TC ((float)0.2236068)
-#define HPDCT_TD ((float)0.70710678)
-inline constexpr Mat64 kBuiltinT = {{
-    HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,  HPDCT_TA,
-    HPDCT_TH,  HPDCT_TH,  0.0f,      0.0f,      0.0f,      0.0f,      -HPDCT_TH, -HPDCT_TH,
-    HPDCT_TB,  HPDCT_TC,  -HPDCT_TC, -HPDCT_TB, -HPDCT_TB, -HPDCT_TC, HPDCT_TC,  HPDCT_TB,
-    0.0f,      0.0f,      -HPDCT_TD, 0.0f,      0.0f,      HPDCT_TD,  0.0f,      0.0f,
-    HPDCT_TA,  -HPDCT_TA, -HPDCT_TA, HPDCT_TA,  HPDCT_TA,  -HPDCT_TA, -HPDCT_TA, HPDCT_TA,
-    HPDCT_TH,  -HPDCT_TH, 0.0f,      0.0f,      0.0f,      0.0f,      HPDCT_TH,  -HPDCT_TH,
-    HPDCT_TC,  -HPDCT_TB, HPDCT_TB,  -HPDCT_TC, -HPDCT_TC, HPDCT_TB,  -HPDCT_TB, HPDCT_TC,
-    0.0f,      0.0f,      0.0f,      -HPDCT_TD, HPDCT_TD,  0.0f,      0.0f,      0.0f}};
-#undef HPDCT_TA
-#undef HPDCT_TH
-#undef HPDCT_TB
-#undef HPDCT_TC
-#undef HPDCT_TD
-
-// JPEG luminance table (main_newAppr.cu:60-68)
-inline constexpr Mat64 kDefaultQ = {{16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
-                                     14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
-                                     18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
-                                     49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99}};
+constexpr Mat64 mat64_of(const float (&a)[64]) {
+    Mat64 m{};
+    for (int i = 0; i < 64; ++i) m.v[i] = a[i];
+    return m;
+}
+inline constexpr Mat64 kBuiltinT = mat64_of(tables::kT);
+inline constexpr Mat64 kDefaultQ = mat64_of(tables::kQ);
 
 // ---------------------------------------------------------------------------
 // Compile-time loop: f(integral_constant<int, I>) for I in [0, N).

@@ -30,6 +30,9 @@ inline bool ends_with(const std::string& s, const char* suf) {
 
 inline bool is_jpeg(const std::string& p) { return ends_with(p, ".jpg") || ends_with(p, ".jpeg"); }
 
+// Largest accepted header field: 2^24 px per side, and w * h below 2^31.
+constexpr int kPgmMaxToken = 1 << 24;
+
 inline int pgm_token(FILE* f) {
     int c = fgetc(f);
     while (c == '#' || c == ' ' || c == '\n' || c == '\r' || c == '\t') {
@@ -40,6 +43,7 @@ inline int pgm_token(FILE* f) {
     int v = 0;
     bool any = false;
     while (c >= '0' && c <= '9') {
+        if (v > kPgmMaxToken / 10) return -1;  // no int overflow on a hostile header (UBSan-checked)
         v = v * 10 + (c - '0');
         any = true;
         c = fgetc(f);
@@ -58,7 +62,7 @@ inline bool load_pgm(const std::string& path, std::vector<uint8_t>& px, int& w, 
     w = pgm_token(f);
     h = pgm_token(f);
     const int maxv = pgm_token(f);
-    if (w <= 0 || h <= 0 || maxv <= 0 || maxv > 255) {
+    if (w <= 0 || h <= 0 || maxv <= 0 || maxv > 255 || (int64_t)w * h >= ((int64_t)1 << 31)) {
         fclose(f);
         return false;
     }

@@ -11,12 +11,19 @@ Sources:
     benchmark_newAppr.cu:46-51.
 The reference ships no fixtures of its own.
 
-Usage: python tests/golden/make_golden.py   (needs oracle built; _ref optional)
+Also: ref_tables.json -- every Q / T table initialiser in the reference's .cu
+sources (quant_matrix / q_matrix / transform_matrix), extracted from the text
+and converted as the reference's compiler does, (float)(double)literal, kept as
+fp32 bit patterns with file:line.  `--tables-only` regenerates just that file.
+
+Usage: python tests/golden/make_golden.py [--tables-only]
+       (needs oracle built and /root/reference present; _ref optional)
 """
 import ctypes
 import hashlib
 import json
 import os
+import re
 import sys
 
 import numpy as np
@@ -37,7 +44,50 @@ def special_floats() -> np.ndarray:
     return np.array(v, np.float32)
 
 
+REFERENCE = "/root/reference"
+TABLE_RE = re.compile(r"float\s+(quant_matrix|q_matrix|transform_matrix)\s*\[[^\]]*\]\s*=\s*\{([^}]*)\}")
+
+
+def extract_tables(root: str = REFERENCE) -> dict:
+    """{"<file>:<line>": {"name", "bits"}} for every table initialiser in the
+    reference's .cu text.  bits[i] = fp32 bit pattern of (float)(double)lit."""
+    out = {}
+    for dirpath, _, files in os.walk(root):
+        if "/.git" in dirpath:
+            continue
+        for fn in sorted(files):
+            if not fn.endswith(".cu"):
+                continue
+            path = os.path.join(dirpath, fn)
+            text = open(path, encoding="utf-8", errors="replace").read()
+            for m in TABLE_RE.finditer(text):
+                lits = [t for t in re.split(r"[\s,]+", m.group(2)) if t]
+                assert len(lits) == 64, (path, m.group(1), len(lits))
+                vals = np.array([np.float32(float(t.rstrip("fF"))) for t in lits], np.float32)
+                line = text.count("\n", 0, m.start()) + 1
+                out[f"{os.path.relpath(path, root)}:{line}"] = {
+                    "name": m.group(1), "bits": [int(b) for b in vals.view(np.uint32)]}
+    return dict(sorted(out.items()))
+
+
+def write_tables() -> None:
+    tabs = extract_tables()
+    assert "main_newAppr.cu:60" in tabs and "main_newAppr.cu:73" in tabs, sorted(tabs)
+    doc = {"generator": "tests/golden/make_golden.py (extract_tables)",
+           "conversion": "(float)(double)literal, as stored by `float x[64] = {...}`",
+           "tables": tabs}
+    with open(os.path.join(HERE, "ref_tables.json"), "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print("wrote", os.path.join(HERE, "ref_tables.json"), len(tabs), "tables")
+
+
 def main() -> None:
+    if os.path.isdir(REFERENCE):
+        write_tables()
+    else:
+        print("/root/reference absent: ref_tables.json NOT regenerated", file=sys.stderr)
+    if "--tables-only" in sys.argv[1:]:
+        return
     manifest = {"generator": "tests/golden/make_golden.py", "seed": 42, "configs": {}}
 
     # C1: 256x256, srand(42) rand()%256 (benchmark_newAppr.cu:44-51)

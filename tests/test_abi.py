@@ -92,6 +92,44 @@ def test_tables_match_reference(hp, oracle):
     assert np.array_equal(hp.default_quant_table(), oracle.default_quant())
 
 
+def ref_tables():
+    """Q / T initialisers extracted from the reference's own .cu text
+    (tests/golden/make_golden.py extract_tables), fp32 bit patterns."""
+    import json
+    doc = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_tables.json")))
+    return {k: np.array(v["bits"], np.uint32) for k, v in doc["tables"].items()}, doc["tables"]
+
+
+def test_tables_pinned_to_reference_text(hp, oracle):
+    """The library's tables (the SAME constexpr arrays the kernels compile to
+    immediates, csrc/hpdct_tables.h) and the oracle's are bit-identical to
+    (float)(double)literal of main_newAppr.cu:60-81 and
+    Benchmark_code/benchmark_newAppr.cu:54-75, and every other table in the
+    reference agrees with them."""
+    bits, meta = ref_tables()
+    q_ref, t_ref = bits["main_newAppr.cu:60"], bits["main_newAppr.cu:73"]
+    assert np.array_equal(bits["Benchmark_code/benchmark_newAppr.cu:54"], q_ref)
+    assert np.array_equal(bits["Benchmark_code/benchmark_newAppr.cu:67"], t_ref)
+    for k, v in bits.items():
+        want = t_ref if meta[k]["name"] == "transform_matrix" else q_ref
+        assert np.array_equal(v, want), k
+    assert np.array_equal(hp.default_transform().reshape(-1).view(np.uint32), t_ref)
+    assert np.array_equal(hp.default_quant_table().reshape(-1).view(np.uint32), q_ref)
+    assert np.array_equal(oracle.default_transform().reshape(-1).view(np.uint32), t_ref)
+    assert np.array_equal(oracle.default_quant().reshape(-1).view(np.uint32), q_ref)
+    assert np.array_equal(hp.get_quant_table().reshape(-1).view(np.uint32), q_ref)
+
+
+def test_kernel_tables_share_one_source():
+    """hpdct_tile.hpp (kernel immediates) and hpdct_api.cpp (host C-ABI) both
+    take the tables from hpdct_tables.h; neither restates a literal."""
+    csrc = os.path.join(ROOT, "cuda-dct-idct_amd", "csrc")
+    for fn in ("hpdct_tile.hpp", "hpdct_api.cpp"):
+        text = open(os.path.join(csrc, fn)).read()
+        assert '#include "hpdct_tables.h"' in text, fn
+        assert "0.35355339" not in text and "121, 120, 101" not in text, fn
+
+
 def test_quant_table_state(hp):
     q = np.arange(1, 65, dtype=np.float32).reshape(8, 8)
     hp.set_quant_table(q)

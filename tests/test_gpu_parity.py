@@ -111,6 +111,29 @@ def test_runtime_transform_equals_builtin(hp, oracle, dev, c1):
     assert bits_equal(a, ref) and bits_equal(b, ref)
 
 
+def test_builtin_immediates_equal_reference_text_tables(hp, dev, c1):
+    """The built-in T (instruction immediates, zero terms skipped) against
+    T and Q as extracted from main_newAppr.cu:60-81's text
+    (tests/golden/ref_tables.json), passed as the caller's T / Q (all 64
+    terms as runtime operands, IEEE division): bit-identical coefficients
+    and reconstructions."""
+    import torch
+    doc = json.load(open(os.path.join(GOLD, "ref_tables.json")))["tables"]
+    T = np.array(doc["main_newAppr.cu:73"]["bits"], np.uint32).view(np.float32).reshape(8, 8)
+    Q = np.array(doc["main_newAppr.cu:60"]["bits"], np.uint32).view(np.float32).reshape(8, 8)
+    builtin = to_host(hp.forward(to_dev(c1, dev)))
+    builtin8 = to_host(hp.forward(to_dev(c1, dev), out_dtype=torch.int8))
+    hp.set_quant_table(Q)
+    try:
+        ext = to_host(hp.forward(to_dev(c1, dev), transform=to_dev(T, dev)))
+        ext_inv = to_host(hp.inverse(to_dev(ext, dev), transform=to_dev(T, dev)))
+    finally:
+        hp.set_quant_table(None)
+    assert bits_equal(builtin, ext)
+    assert np.array_equal(builtin8.astype(np.float32), ext)
+    assert bits_equal(to_host(hp.inverse(to_dev(builtin, dev))), ext_inv)
+
+
 def test_custom_transform_and_quant(hp, oracle, dev, c1):
     rng = np.random.default_rng(5)
     T = np.linalg.qr(rng.standard_normal((8, 8)))[0].astype(np.float32)
