@@ -11,10 +11,9 @@
 //     bytes (8 per set),
 //   - each fp32 row store is two global_store_dwordx4 that together cover
 //     2 KiB contiguous.
-// Persistent variant (kVarPersist): a grid of resident waves walks the sets
-// with stride = number of waves, and issues the loads of its next set before
-// computing the current one, so HBM reads overlap the VALU work instead of
-// every wave loading, then computing, then storing in lock-step.
+// Only the variants the library launches live here (hpdct_launch.hpp); the
+// measured-and-rejected A/B variants and the phase-split diagnostics are in
+// the tools-only tools/kbench_variants.hpp.
 // Why not one wavefront per tile: a lane-per-pixel mapping needs 7 cross-lane
 // operands per output per pass (14 DPP/ds_bpermute per pixel), which on its
 // own costs as much LDS-crossbar time as the whole HBM stream; see DESIGN.md.
@@ -25,55 +24,26 @@
 
 namespace hpdct {
 
-// Compile-time kernel variants (bit flags).
+// Compile-time kernel variants (bit flags) of the product kernels.  Bits not
+// listed here are the tools' A/B variants (tools/kbench_variants.hpp).
 enum : unsigned {
     kVarFastDiv = 1u,  // quotient by  q0=c*r; e=fma(-q0,Q,c); q=fma(e,r,q0)  (r = RN(1/Q)).  Gives the same
                        // roundf() as IEEE c/Q for every |c| <= 4096 and every integer Q in 1..255
                        // (exhaustive: tests/tools/verify_fastdiv.*); only enabled for such tables and
                        // uint8 input with the built-in T (|C| <= 1024).
-    kVarPersist = 2u,  // persistent waves + prefetch of the next tile set
-    kVarXorCvt = 4u,   // uint8 -> (x - 128) as (float)(int8_t)(b ^ 0x80): one XOR per 4 pixels + one
-                       // sign-extending byte convert per pixel instead of convert + subtract
     kVarLdsStore = 8u, // fp32 rows re-staged through LDS so every store instruction writes 1 KiB contiguous
     kVarNT = 16u,      // non-temporal (streaming) stores for the output planes
-    kVarRowMajor = 32u,  // forward: finish each P row and its C row before the next (fewer live VGPRs?)
-    kVarLdsSwz = 64u,    // LDS re-staging with the slot swizzle k ^ ((k >> 3) & 1): conflict-free deposits
-    kVarLdsLoad = 128u,  // fp32 inputs: 1 KiB-contiguous row loads, re-staged through LDS into the tile layout
-    // bits 8..11: minimum waves per SIMD requested from the register allocator (0 = compiler default)
     // bits 12..13: workgroup size: 0 -> 256 threads, 1 -> 64, 2 -> 512, 3 -> 1024
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
-    kVarNTLoad = 1u << 16,    // non-temporal loads of the 8-bit input planes
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
-    kVarPersist2 = 1u << 22,    // persistent waves, next set prefetched under a wave-uniform branch only
-                                // (per-lane addresses clamped instead of divergent loads), so the
-                                // compute of set n overlaps the loads of set n+1
-    kVarTwoSets = 1u << 23,     // each wave takes two consecutive sets, all 16 row loads issued up front:
-                                // the first set's compute overlaps the second set's loads
-    kVarStSc1 = 1u << 24,       // fp32 re-staged stores as global_store_dwordx4 ... sc1 (with kVarNT: sc1 nt)
-    kVarStSc0Sc1 = 1u << 25,    // ... sc0 sc1 (with kVarNT: sc0 sc1 nt)
-    kVarPacked = 1u << 19,      // uint8 input, built-in T, quantised: packed-fp32 transform and quotient
-                                // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, fdct_tile_pk)
-    kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
-                                // all finite -> the zero terms of T are skipped (exact: a chain from +0
-                                // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
-    kVarPrio = 1u << 26,        // s_setprio 3 while the wave computes its addresses and issues its loads
-    // diagnostics only (tools/kbench): split the kernel's time into its phases
-    kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
-    kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
-                                // over the 8 XCDs; remap so XCD x walks one contiguous 1/8 of the sets
-    kVarNoStore = 1u << 28,
-    kVarPanel = 1u << 31,       // wide frames (tiles_x a multiple of 512, > 512): sets walk 4096-px-wide
-                                // column panels top to bottom, panel after panel, instead of whole rows
-    kVarStraddle = 1u << 30,    // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
-                                // multiple of 512 px) stores two contiguous runs per instruction instead of
-                                // 32 B per lane; launched only for such widths (the branch costs the
-                                // power-of-two frames ~3 %, profiles/r01/ab_straddle.log)     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
+    kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
+                              // multiple of 512 px) stores two contiguous runs per instruction instead of
+                              // 32 B per lane; launched only for such widths (the branch costs the
+                              // power-of-two frames ~3 %, profiles/r01/ab_straddle.log)
 };
-template <unsigned kVar>
-constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
 template <unsigned kVar>
 constexpr uint32_t kBlock = ((kVar >> 12) & 3u) == 1u   ? 64u
                             : ((kVar >> 12) & 3u) == 2u ? 512u
@@ -212,20 +182,8 @@ struct RawTile;
 template <>
 struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
     uint2 r[8];
-    // an empty asm that consumes every register: the loads must have landed
-    // here (persistent walk: keeps the wait out of the pipelined loop)
-    __device__ __forceinline__ void settle() {
-        unroll<8>([&](auto i) { asm volatile("" : "+v"(r[i].x), "+v"(r[i].y)); });
-    }
     __device__ __forceinline__ void load(const uint8_t* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
-    }
-    __device__ __forceinline__ void load_nt(const uint8_t* __restrict__ p, uint64_t width) {
-        unroll<8>([&](auto i) {
-            const uint2* q = reinterpret_cast<const uint2*>(p + i * width);
-            r[i].x = __builtin_nontemporal_load(&q->x);
-            r[i].y = __builtin_nontemporal_load(&q->y);
-        });
     }
     __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
         unroll<8>([&](auto i) {
@@ -250,9 +208,6 @@ struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
 template <>
 struct RawTile<int8_t> {  // int8 coefficients, 16 VGPRs
     uint2 r[8];
-    __device__ __forceinline__ void settle() {
-        unroll<8>([&](auto i) { asm volatile("" : "+v"(r[i].x), "+v"(r[i].y)); });
-    }
     __device__ __forceinline__ void load(const int8_t* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(p + i * width); });
     }
@@ -267,39 +222,13 @@ struct RawTile<int8_t> {  // int8 coefficients, 16 VGPRs
 };
 
 template <>
-struct RawTile<float> {
-    __device__ __forceinline__ void settle() {
-        unroll<16>([&](auto n) {
-            float4& v = r[n / 2][n % 2];
-            asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
-        });
-    }  // 64 VGPRs
+struct RawTile<float> {  // 64 VGPRs
     float4 r[8][2];
     __device__ __forceinline__ void load(const float* __restrict__ p, uint64_t width) {
         unroll<8>([&](auto i) {
             const float4* src = reinterpret_cast<const float4*>(p + i * width);
             r[i][0] = src[0];
             r[i][1] = src[1];
-        });
-    }
-    // Whole 64-tile set in one tile row: lane j loads 16 B at [16j, 16j+16) and
-    // [1024+16j, ...) of each 2 KiB row segment (two 1 KiB-contiguous loads per
-    // row), the rows pass through the wave's LDS slots and every lane picks up
-    // its own tile's 32 B.  In-order LDS within one wave: no barrier.
-    __device__ __forceinline__ void load_staged(const float* __restrict__ seg, uint64_t width, uint32_t lane,
-                                                float4* __restrict__ slots) {
-        float4 a[8], b[8];
-        unroll<8>([&](auto i) {
-            const float4* src = reinterpret_cast<const float4*>(seg + i * width);
-            a[i] = src[lane];
-            b[i] = src[64 + lane];
-        });
-        unroll<8>([&](auto i) {
-            float4* slot = slots + (i & 1) * 128;
-            slot[lane] = a[i];
-            slot[64 + lane] = b[i];
-            r[i][0] = slot[2 * lane];
-            r[i][1] = slot[2 * lane + 1];
         });
     }
     __device__ __forceinline__ void to_float(float (&x)[8][8], float shift) const {
@@ -360,37 +289,25 @@ __device__ __forceinline__ void store_row(TOut* __restrict__ row, const float (&
 // first tile), i.e. two stores of 1 KiB contiguous each.  LDS accesses of
 // one wave execute in order, so no barrier is needed between deposit and
 // pick-up; the slot alternates with the row parity to let them overlap.
-// Optional slot swizzle sw(k) = k ^ ((k >> 3) & 1) (an involution that keeps
-// [0,64) and [64,128)): the deposits of 8 consecutive lanes then hit 8
-// distinct 16-B bank groups; the pick-up of slot j stores to position sw(j).
-// 16-byte store with an explicit cache policy (kPol: 0 = st<kNT>, 1 = sc1,
-// 2 = sc0 sc1; kNT adds nt) through a raw buffer store, whose aux operand
-// carries the gfx940+ cache-policy bits (sc0 = 1, nt = 2, sc1 = 16); inline
-// asm is not an option: the compiler would not track the store's read of its
-// data registers.  `base` is wave-uniform, `off` the lane's byte offset.
-template <bool kNT, int kPol>
-__device__ __forceinline__ void st_pol(float* base, uint32_t off, const float4& v) {
-    if constexpr (kPol == 0) {
-        st<kNT>(reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + off), v);
-    } else {
-        constexpr int kAux = (kPol == 1 ? 16 : 17) | (kNT ? 2 : 0);
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-        const v4i w = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(w, rsrc, off, 0, kAux);
-    }
+// 16-byte store at a byte offset from a wave-uniform base
+template <bool kNT>
+__device__ __forceinline__ void st_at(float* base, uint32_t off, const float4& v) {
+    st<kNT>(reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + off), v);
 }
 
-template <bool kNT, bool kSwz, int kPol = 0>
+template <bool kNT>
 __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* __restrict__ seg, uint32_t lane,
                                               const float (&c)[8]) {
-    auto sw = [](uint32_t k) { return kSwz ? (k ^ ((k >> 3) & 1u)) : k; };
-    slot[sw(2 * lane)] = make_float4(c[0], c[1], c[2], c[3]);
-    slot[sw(2 * lane + 1)] = make_float4(c[4], c[5], c[6], c[7]);
+    // slot index map (identity).  Written as a call on purpose: with the plain
+    // expressions hipcc (ROCm 7.2) schedules the 64-bit address arithmetic of
+    // the stores differently and the headline kernel grows by 29 instructions.
+    auto ix = [](uint32_t k) { return k; };
+    slot[ix(2 * lane)] = make_float4(c[0], c[1], c[2], c[3]);
+    slot[ix(2 * lane + 1)] = make_float4(c[4], c[5], c[6], c[7]);
     const float4 a = slot[lane];
     const float4 b = slot[64 + lane];
-    st_pol<kNT, kPol>(seg, 16u * sw(lane), a);
-    st_pol<kNT, kPol>(seg, 16u * (64u + sw(lane)), b);
+    st_at<kNT>(seg, 16u * ix(lane), a);
+    st_at<kNT>(seg, 16u * (64u + ix(lane)), b);
 }
 
 // The same for a set that straddles a tile-row boundary (ragged widths): its
@@ -411,8 +328,7 @@ __device__ __forceinline__ void store_row_lds2(float4* __restrict__ slot, float*
     st<kNT>(reinterpret_cast<float4*>(q1 < h ? seg + 4u * q1 : seg2 + 4u * (q1 - h)), b);
 }
 
-// Per-wave walk over 64-tile sets: one set per wave (plain), or a grid-stride
-// loop with the next set's loads issued before the current set's compute.
+// Per-wave walk over 64-tile sets: one set per wave, wave w = set w.
 // body(raw, p, split, seg): split (wave-uniform) = 64 when the whole set is 64
 // valid tiles of one tile row, whose row segments start at element seg; k in
 // 1..63 when the set is 64 valid tiles whose first k end one tile row (at seg)
@@ -420,15 +336,9 @@ __device__ __forceinline__ void store_row_lds2(float4* __restrict__ slot, float*
 // ragged last set or a set over more than two tile rows (per-lane stores).
 template <unsigned kVar, typename TIn, typename Body>
 __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const TileGrid& g, float4* slots, Body&& body) {
-    constexpr bool kPersist = (kVar & kVarPersist) != 0;
+    (void)slots;
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t block = blockIdx.x;
-    if constexpr ((kVar & kVarXcdSwz) != 0) {
-        // bijective: XCD x = block % 8 owns q (+1 for x < r) consecutive blocks
-        const uint32_t nb = gridDim.x, q = nb / 8u, r = nb % 8u, x = block % 8u;
-        block = x * q + (x < r ? x : r) + block / 8u;
-    }
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(block * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t nsets = (g.ntiles + 63u) / 64u;
     auto seg_info = [&](uint32_t set, const TilePos& p, uint64_t& seg) -> uint32_t {
         const uint32_t t0 = set * 64u;
@@ -450,120 +360,16 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         seg = static_cast<uint64_t>(ty0) * 8u * g.width + static_cast<uint64_t>(tx0) * 8u;
         return 64u - k <= g.tiles_x ? k : 0u;
     };
-    if constexpr ((kVar & kVarTwoSets) != 0) {
-        const uint32_t s0 = wave * 2u;
-        if (s0 >= nsets) return;
-        auto clamp_tile = [&](uint32_t s_) {
-            uint32_t t = s_ * 64u + lane;
-            return t < g.ntiles ? t : g.ntiles - 1u;  // lanes past the end redo the last tile (same bytes)
-        };
-        RawTile<TIn> a, b;
-        const TilePos pa = tile_pos(g, clamp_tile(s0)), pb = tile_pos(g, clamp_tile(s0 + 1u));
-        a.load(src + pa.base, g.width);
-        b.load(src + pb.base, g.width);
-        uint64_t seg;
-        uint32_t ok = seg_info(s0, pa, seg);
-        body(a, pa, ok, seg);
-        if (s0 + 1u < nsets) {  // wave-uniform
-            ok = seg_info(s0 + 1u, pb, seg);
-            body(b, pb, ok, seg);
-        }
-    } else if constexpr ((kVar & kVarPersist2) != 0) {
-        const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
-        uint32_t set = wave;
-        if (set >= nsets) return;
-        auto load_set = [&](RawTile<TIn>& r, uint32_t s_) {
-            uint32_t t = s_ * 64u + lane;
-            if (t >= g.ntiles) t = g.ntiles - 1u;  // clamp: every lane loads, no divergent load
-            r.load(src + tile_pos(g, t).base, g.width);
-        };
-        RawTile<TIn> cur;
-        load_set(cur, set);
-        cur.settle();  // first set waited here, once: no load of it is pending at the loop header
-        while (true) {
-            const uint32_t nset = set + nwaves;
-            const bool more = nset < nsets;  // wave-uniform
-            RawTile<TIn> nxt;
-            if (more) load_set(nxt, nset);
-            // lanes past the last tile run the body on their clamped tile (the
-            // last valid one): they store byte-identical values to the same
-            // addresses, so the loop body has no divergent branch and the
-            // wait for the next set's loads does not have to drain the stores
-            uint32_t t = set * 64u + lane;
-            if (t >= g.ntiles) t = g.ntiles - 1u;
-            const TilePos p = tile_pos(g, t);
-            uint64_t seg;
-            const uint32_t ok = seg_info(set, p, seg);
-            body(cur, p, ok, seg);
-            if (!more) break;
-            cur = nxt;
-            set = nset;
-        }
-    } else if constexpr (!kPersist) {
-        if (wave >= nsets) return;
-        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(3);
-        TilePos p;
-        uint64_t seg;
-        uint32_t ok;
-        constexpr uint32_t kPanelTiles = 512u;
-        if ((kVar & kVarPanel) != 0 && g.tiles_x % kPanelTiles == 0u && g.tiles_x > kPanelTiles) {
-            // set -> (panel, tile row, 64-tile chunk): every set is 64 tiles of one tile row
-            constexpr uint32_t kSpr = kPanelTiles / 64u;
-            const uint32_t per_panel = kSpr * (g.ntiles / g.tiles_x);
-            const uint32_t pn = wave / per_panel, r = wave - pn * per_panel;
-            const uint32_t ty = r / kSpr, cx = r - ty * kSpr;
-            p.valid = true;
-            seg = static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(pn * kPanelTiles + cx * 64u) * 8u;
-            p.base = seg + 8u * static_cast<uint64_t>(lane);
-            ok = 64u;
-        } else {
-            p = tile_pos(g, wave * 64u + lane);
-            ok = seg_info(wave, p, seg);
-        }
-        if (!p.valid) return;
-        RawTile<TIn> raw;
-        if constexpr ((kVar & kVarNoLoad) != 0 && sizeof(TIn) == 1) {
-            unroll<8>([&](auto i) {
-                raw.r[i] = make_uint2((lane * 0x01010101u) ^ (i * 0x10325476u), (lane * 0x03050709u) + i);
-            });
-        } else if constexpr ((kVar & kVarLdsLoad) != 0 && std::is_same_v<TIn, float>) {
-            if (ok == 64u) {
-                raw.load_staged(src + seg, g.width, lane, slots);
-            } else {
-                raw.load(src + p.base, g.width);
-            }
-        } else if constexpr ((kVar & kVarNTLoad) != 0 && std::is_same_v<TIn, uint8_t>) {
-            raw.load_nt(src + p.base, g.width);
-        } else {
-            raw.load(src + p.base, g.width);
-        }
-        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(0);
-        body(raw, p, ok, seg);
-    } else {
-        const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);
-        uint32_t set = wave;
-        if (set >= nsets) return;
-        TilePos p = tile_pos(g, set * 64u + lane);
-        RawTile<TIn> cur;
-        if (p.valid) cur.load(src + p.base, g.width);
-        while (true) {
-            const uint32_t nset = set + nwaves;
-            const bool more = nset < nsets;  // wave-uniform
-            TilePos np = p;
-            RawTile<TIn> nxt;
-            if (more) {
-                np = tile_pos(g, nset * 64u + lane);
-                if (np.valid) nxt.load(src + np.base, g.width);
-            }
-            uint64_t seg;
-            const uint32_t ok = seg_info(set, p, seg);
-            if (p.valid) body(cur, p, ok, seg);
-            if (!more) break;
-            cur = nxt;
-            p = np;
-            set = nset;
-        }
-    }
+    if (wave >= nsets) return;
+    TilePos p;
+    uint64_t seg;
+    uint32_t ok;
+    p = tile_pos(g, wave * 64u + lane);
+    ok = seg_info(wave, p, seg);
+    if (!p.valid) return;
+    RawTile<TIn> raw;
+    raw.load(src + p.base, g.width);
+    body(raw, p, ok, seg);
 }
 
 // Emits one row of 8 values for the lane's tile: through the LDS re-staging
@@ -581,9 +387,7 @@ struct RowSink {
                                                const float (&c)[8]) const {
         if constexpr (kLds) {
             if (split == 64u) {
-                constexpr int kPol = (kVar & kVarStSc1) ? 1 : (kVar & kVarStSc0Sc1) ? 2 : 0;
-                store_row_lds<kNT, (kVar & kVarLdsSwz) != 0, kPol>(slots + (v & 1) * 128,
-                                                                   plane + seg + v * width, threadIdx.x & 63u, c);
+                store_row_lds<kNT>(slots + (v & 1) * 128, plane + seg + v * width, threadIdx.x & 63u, c);
                 return;
             }
             if ((kVar & kVarStraddle) != 0 && split != 0u) {
@@ -598,10 +402,10 @@ struct RowSink {
     }
 };
 
-// The wave's two 2 KiB LDS slots (used by the store and load re-staging).
+// The wave's two 2 KiB LDS slots (the store re-staging).
 template <unsigned kVar>
 __device__ __forceinline__ float4* wave_slots() {
-    if constexpr ((kVar & (kVarLdsStore | kVarLdsLoad)) != 0) {
+    if constexpr ((kVar & kVarLdsStore) != 0) {
         __shared__ float4 stage[kBlock<kVar> / 64u][2 * 128];
         return stage[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
     } else {
@@ -609,7 +413,7 @@ __device__ __forceinline__ float4* wave_slots() {
     }
 }
 
-// kVarFiniteSkip: true (wave-uniform) when every live lane's tile holds only
+// true (wave-uniform) when every live lane's tile holds only
 // values with |v| < 2^125.  Then no operand is inf/NaN and no partial sum of
 // the first pass can overflow (|T row|_1 <= 8 * 0.7072 < 8), so the
 // products by the zero entries of T contribute exactly +0 to chains that
@@ -629,10 +433,9 @@ __device__ __forceinline__ bool wave_tame(const float (&x)[8][8]) {
 // Forward: image -> (quantised) coefficients.
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
-__global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
-                                                             float* __restrict__ shifted, TileGrid g,
-                                                             const float* __restrict__ t_dev, QParams qp,
-                                                             float shift) {
+__global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
+                                                            float* __restrict__ shifted, TileGrid g,
+                                                            const float* __restrict__ t_dev, QParams qp, float shift) {
     // finite inputs (u8) may skip the zero terms of the built-in T
     constexpr bool kSkipZero = std::is_same_v<TIn, uint8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
@@ -640,60 +443,9 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     const RowSink<kVar, float> wb_sink{shifted, g.width, slots};
 
-    walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok,
-                                                      uint64_t seg) {
-        if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && kBuiltinT && kQuant &&
-                      !kWriteback && (kVar & kVarRowFirst) == 0) {
-            float xs[8][8];
-            raw.to_float(xs, 0.0f);
-            f32x2 x2[8][4];
-            unroll<8>([&](auto i) {
-                unroll<4>([&](auto cp) { x2[i][cp] = f32x2{xs[i][2 * cp], xs[i][2 * cp + 1]} - f32x2{shift, shift}; });
-            });
-            fdct_tile_pk(x2, [&](auto v, f32x2(&c2)[4]) {
-                // quotient per pair: the verified 3-op form (packed) or IEEE division
-                f32x2 d2[4];
-                unroll<4>([&](auto k) {
-                    constexpr int u0 = kPairU[k][0], u1 = kPairU[k][1];
-                    const f32x2 q2 = {qp.q.v[v * 8 + u0], qp.q.v[v * 8 + u1]};
-                    if constexpr ((kVar & kVarFastDiv) != 0) {
-                        const f32x2 r2 = {qp.r.v[v * 8 + u0], qp.r.v[v * 8 + u1]};
-                        const f32x2 q0 = c2[k] * r2;
-                        const f32x2 e = fma2(-q0, q2, c2[k]);
-                        d2[k] = fma2(e, r2, q0);
-                    } else {
-                        d2[k] = f32x2{c2[k].x / q2.x, c2[k].y / q2.y};
-                    }
-                    // round half away: trunc(d + copysign(0.49999997, d)) (verify_round3.c)
-                    d2[k] = d2[k] + f32x2{__builtin_copysignf(0.49999997f, d2[k].x),
-                                          __builtin_copysignf(0.49999997f, d2[k].y)};
-                });
-                if constexpr (std::is_same_v<TOut, int8_t>) {
-                    uint32_t w[2] = {0u, 0u};
-                    unroll<4>([&](auto k) {
-                        constexpr int u0 = kPairU[k][0], u1 = kPairU[k][1];
-                        cvt_into_byte<u0 % 4>(w[u0 / 4], d2[k].x);
-                        cvt_into_byte<u1 % 4>(w[u1 / 4], d2[k].y);
-                    });
-                    st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width),
-                                             make_uint2(w[0], w[1]));
-                } else {
-                    float c[8];
-                    unroll<4>([&](auto k) {
-                        c[kPairU[k][0]] = __builtin_truncf(d2[k].x);
-                        c[kPairU[k][1]] = __builtin_truncf(d2[k].y);
-                    });
-                    sink(v, p, ok, seg, c);
-                }
-            });
-            return;
-        }
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         float x[8][8];
-        if constexpr ((kVar & kVarXorCvt) != 0 && std::is_same_v<TIn, uint8_t>) {
-            raw.to_float_minus128(x);  // launcher guarantees shift == 128
-        } else {
-            raw.to_float(x, shift);
-        }
+        raw.to_float(x, shift);
         if constexpr (kWriteback) {
             // the reference leaves X-128 in its input (main_newAppr.cu:273)
             unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
@@ -702,9 +454,6 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
             if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
                 unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
                 const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
-                if constexpr ((kVar & kVarNoStore) != 0) {
-                    if (g.ntiles != 0xffffffffu) return;
-                }
                 st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
                 return;
             }
@@ -715,14 +464,8 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
         };
         if constexpr ((kVar & kVarRowFirst) != 0) {
             fdct_tile_rowfirst(T, x, emit);
-        } else if constexpr ((kVar & kVarFiniteSkip) != 0 && kBuiltinT && !kSkipZero) {
-            if (wave_tame(x)) {
-                fdct_tile<(kVar & kVarRowMajor) != 0>(TSource<true, true>(t_dev), x, emit);
-            } else {
-                fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, emit);
-            }
         } else {
-            fdct_tile<(kVar & kVarRowMajor) != 0>(T, x, emit);
+            fdct_tile(T, x, emit);
         }
     });
 }
@@ -731,17 +474,16 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void fdct_kernel(con
 // Inverse: (quantised) coefficients -> image.
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kDequant, bool kBuiltinT, unsigned kVar>
-__global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
-                                                             float* __restrict__ dq_out, TileGrid g,
-                                                             const float* __restrict__ t_dev, Mat64 q, float shift) {
+__global__ __launch_bounds__(kBlock<kVar>, 1) void idct_kernel(const TIn* __restrict__ coef, TOut* __restrict__ out,
+                                                            float* __restrict__ dq_out, TileGrid g,
+                                                            const float* __restrict__ t_dev, Mat64 q, float shift) {
     constexpr bool kSkipZero = std::is_same_v<TIn, int8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     const RowSink<kVar, float> dq_sink{dq_out, g.width, slots};
 
-    walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok,
-                                                       uint64_t seg) {
+    walk_sets<kVar>(coef, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         float d[8][8];
         raw.to_float(d, 0.0f);
         if constexpr (kDequant) {
@@ -758,12 +500,6 @@ __global__ __launch_bounds__(kBlock<kVar>, kMinWaves<kVar>) void idct_kernel(con
         };
         if constexpr ((kVar & kVarRowFirst) != 0) {
             idct_tile_rowfirst(T, d, emit);
-        } else if constexpr ((kVar & kVarFiniteSkip) != 0 && kBuiltinT && !kSkipZero) {
-            if (wave_tame(d)) {
-                idct_tile(TSource<true, true>(t_dev), d, emit);
-            } else {
-                idct_tile(T, d, emit);
-            }
         } else {
             idct_tile(T, d, emit);
         }
@@ -780,7 +516,7 @@ __device__ __forceinline__ uint32_t hash_px(uint64_t seed, uint64_t idx) {
     return static_cast<uint32_t>((z ^ (z >> 31)) & 255u);
 }
 
-static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t* __restrict__ out, uint64_t n,
+[[maybe_unused]] static __global__ __launch_bounds__(kBlockThreads) void fill_hash_kernel(uint8_t* __restrict__ out, uint64_t n,
                                                                          uint64_t seed, uint64_t first) {
     const uint64_t i0 = (static_cast<uint64_t>(blockIdx.x) * kBlockThreads + threadIdx.x) * 16u;
     if (i0 >= n) return;

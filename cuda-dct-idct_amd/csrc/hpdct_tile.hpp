@@ -94,26 +94,8 @@ struct TSource {
 // Forward tile transform on registers: x[i][j] level-shifted pixels,
 // returns P via the column pass, then calls emit(v, c[8]) for each output row
 // (so each row can be quantised and stored while the next is computed).
-template <bool kRowMajor = false, typename TS, typename Emit>
+template <typename TS, typename Emit>
 __device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& emit) {
-    if constexpr (kRowMajor) {
-        // same chains, P row v and C row v finished before row v+1
-        unroll<8>([&](auto v) {
-            float p[8], c[8];
-            unroll<8>([&](auto col) {
-                float s = 0.0f;
-                unroll<8>([&](auto i) { s = T.template mac<v * 8 + i>(x[i][col], s); });
-                p[col] = s;
-            });
-            unroll<8>([&](auto u) {
-                float s = 0.0f;
-                unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(p[i], s); });
-                c[u] = s;
-            });
-            emit(v, c);
-        });
-        return;
-    }
     float p[8][8];
     // P = T . X   (main_newAppr.cu:193-197): P[v][col] = sum_i T[v][i] X[i][col]
     unroll<8>([&](auto col) {
@@ -202,53 +184,6 @@ __device__ __forceinline__ void idct_tile(const TS& T, float (&d)[8][8], Emit&& 
             r[u] = s;
         });
         emit(v, r);
-    });
-}
-
-// ---------------------------------------------------------------------------
-// Packed-fp32 forward (v_pk_fma_f32: two IEEE fmas per instruction, each half
-// rounded exactly like the scalar v_fma_f32), built-in T, finite inputs.
-//   pass 1: pairs of columns, T[v][i] broadcast:
-//           p2[v][cp] = {P[v][2cp], P[v][2cp+1]}, the same chains as fdct_tile.
-//   pass 2: pairs of output columns (u0, u1) chosen so that T's zero patterns
-//           coincide -- (0,2) (4,6) full rows, (1,5) and (3,7) zero at the same
-//           i (3,7 at i=0,1,6,7) -- and the terms where both are zero are
-//           skipped; a term zero in one half only adds fma(0, P, s) = s
-//           exactly (P finite, s never -0), so each half equals the scalar chain.
-// emit2(v, c2) receives c2[k] = {C[v][kPairU[k][0]], C[v][kPairU[k][1]]}.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-inline constexpr int kPairU[4][2] = {{0, 2}, {4, 6}, {1, 5}, {3, 7}};
-
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-template <typename Emit2>
-__device__ __forceinline__ void fdct_tile_pk(const f32x2 (&x2)[8][4], Emit2&& emit2) {
-    f32x2 p2[8][4];
-    unroll<8>([&](auto v) {
-        unroll<4>([&](auto cp) {
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float c = kBuiltinT.v[v * 8 + i];
-                if constexpr (c != 0.0f) s = fma2(f32x2{c, c}, x2[i][cp], s);
-            });
-            p2[v][cp] = s;
-        });
-    });
-    unroll<8>([&](auto v) {
-        f32x2 c2[4];
-        unroll<4>([&](auto k) {
-            constexpr int u0 = kPairU[k][0], u1 = kPairU[k][1];
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float a = kBuiltinT.v[u0 * 8 + i], b = kBuiltinT.v[u1 * 8 + i];
-                if constexpr (a != 0.0f || b != 0.0f) {
-                    const float pv = p2[v][i / 2][i % 2];
-                    s = fma2(f32x2{a, b}, f32x2{pv, pv}, s);
-                }
-            });
-            c2[k] = s;
-        });
-        emit2(v, c2);
     });
 }
 

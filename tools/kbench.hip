@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "hpdct_launch.hpp"
+#include "kbench_variants.hpp"
 #include "hpdct_duo.hpp"
 
 using namespace hpdct;
@@ -141,8 +142,8 @@ struct Variant {
 
 template <unsigned kVar>
 void launch_var(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus, hipStream_t s) {
-    const dim3 grid = grid_for(g, (kVar & kVarPersist) != 0, cus, kBlock<kVar>);
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), grid, dim3(kBlock<kVar>), 0, s, in,
+    const dim3 grid = grid_for(g, (kVar & ab::kVarPersist) != 0, cus, kBlock<kVar>);
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar>), grid, dim3(kBlock<kVar>), 0, s, in,
                        out, nullptr, g, nullptr, qp, 128.0f);
 }
 
@@ -151,7 +152,7 @@ void launch_var_occ(const uint8_t* in, float* out, const TileGrid& g, const QPar
                     hipStream_t s) {
     const uint32_t sets = (g.ntiles + 63u) / 64u;
     uint32_t blocks = std::min<uint32_t>((sets + 3) / 4, cus * kWavesPerCU / 4);
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), dim3(blocks), dim3(kBlockThreads), 0,
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar>), dim3(blocks), dim3(kBlockThreads), 0,
                        s, in, out, nullptr, g, nullptr, qp, 128.0f);
 }
 
@@ -160,7 +161,7 @@ void launch_var_occ(const uint8_t* in, float* out, const TileGrid& g, const QPar
 template <typename TI, typename TO, unsigned kVar>
 void launch_fwd_any(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                     hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, false, cus, kBlock<kVar>),
+    hipLaunchKernelGGL((ab::fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, false, cus, kBlock<kVar>),
                        dim3(kBlock<kVar>),
                        0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr, g, nullptr, qp,
                        128.0f);
@@ -168,7 +169,7 @@ void launch_fwd_any(const uint8_t* in, float* out, const TileGrid& g, const QPar
 template <typename TI, typename TO, unsigned kVar>
 void launch_inv_any(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                     hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<TI, TO, true, true, kVar>), grid_for(g, false, cus, kBlock<kVar>),
+    hipLaunchKernelGGL((ab::idct_kernel<TI, TO, true, true, kVar>), grid_for(g, false, cus, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr, g, nullptr, qp.q, 128.0f);
 }
@@ -192,7 +193,7 @@ float* g_wb = nullptr;
 template <unsigned kVar>
 void launch_fwd_compat_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
                             hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<float, float, true, false, true, kVar>), grid_for(g, false, 0, kBlock<kVar>),
+    hipLaunchKernelGGL((ab::fdct_kernel<float, float, true, false, true, kVar>), grid_for(g, false, 0, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s, reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
 }
 template <unsigned kVar>
@@ -211,7 +212,7 @@ void launch_fwd_compat_oct(const uint8_t* in, float* out, const TileGrid& g, con
 template <unsigned kVar>
 void launch_cublas_fwd_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
                             hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<float, float, true, false, true, kVar | kVarRowFirst>),
+    hipLaunchKernelGGL((ab::fdct_kernel<float, float, true, false, true, kVar | kVarRowFirst>),
                        grid_for(g, false, 0, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp, 128.0f);
 }
@@ -224,7 +225,7 @@ void launch_cublas_fwd_duo(const uint8_t* in, float* out, const TileGrid& g, con
 template <unsigned kVar>
 void launch_cublas_inv_tile(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t,
                             hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<float, float, true, false, kVar | kVarRowFirst | kVarWbDequant>),
+    hipLaunchKernelGGL((ab::idct_kernel<float, float, true, false, kVar | kVarRowFirst | kVarWbDequant>),
                        grid_for(g, false, 0, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        reinterpret_cast<const float*>(in), out, g_wb, g, g_T, qp.q, 128.0f);
 }
@@ -253,7 +254,7 @@ void launch_inv_duo(const uint8_t* in, float* out, const TileGrid& g, const QPar
 template <typename TI, typename TO, unsigned kVar>
 void launch_fwd_pers(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                      hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, true, cus, kBlock<kVar>),
+    hipLaunchKernelGGL((ab::fdct_kernel<TI, TO, true, true, false, kVar>), grid_for(g, true, cus, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s, reinterpret_cast<const TI*>(in), reinterpret_cast<TO*>(out), nullptr,
                        g, nullptr, qp, 128.0f);
 }
@@ -289,20 +290,20 @@ void launch_i8_pers_w(const uint8_t* in, float* out, const TileGrid& g, const QP
     const uint32_t per = kBlock<kVar> / 64u;
     const uint32_t sets = (g.ntiles + 63u) / 64u;
     const uint32_t blocks = std::min<uint32_t>((sets + per - 1) / per, cus * kW / per);
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(blocks), dim3(kBlock<kVar>), 0,
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(blocks), dim3(kBlock<kVar>), 0,
                        s, in, reinterpret_cast<int8_t*>(out), nullptr, g, nullptr, qp, 128.0f);
 }
 
 template <unsigned kVar>
 void launch_i8_two(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
     const uint32_t sets = (g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
                        dim3(kBlock<kVar>), 0, s, in, reinterpret_cast<int8_t*>(out), nullptr, g, nullptr, qp, 128.0f);
 }
 template <unsigned kVar>
 void launch_f32_two(const uint8_t* in, float* out, const TileGrid& g, const QParams& qp, uint32_t, hipStream_t s) {
     const uint32_t sets = (g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar>), dim3(((sets + 1) / 2 + per - 1) / per),
                        dim3(kBlock<kVar>), 0, s, in, out, nullptr, g, nullptr, qp, 128.0f);
 }
 
@@ -356,23 +357,23 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&inf[s], px * 4));
         CK(hipMemcpy(inf[s], hf.data(), px * 4, hipMemcpyHostToDevice));
     }
-    constexpr unsigned F = kVarFastDiv, X = kVarXorCvt, L = kVarLdsStore, N = kVarNT, P = kVarPersist;
-    constexpr unsigned B = L | N | F, R = kVarRowMajor, S = kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
-    constexpr unsigned LL = kVarLdsLoad;
-    constexpr unsigned NL = kVarNTLoad, IP = kVarI8Pack;
-    constexpr unsigned PK = kVarPacked, OR = kOctRestage;
+    constexpr unsigned F = kVarFastDiv, X = ab::kVarXorCvt, L = kVarLdsStore, N = kVarNT, P = ab::kVarPersist;
+    constexpr unsigned B = L | N | F, R = ab::kVarRowMajor, S = ab::kVarLdsSwz, W512 = 2u << 12, W1024 = 3u << 12;
+    constexpr unsigned LL = ab::kVarLdsLoad;
+    constexpr unsigned NL = ab::kVarNTLoad, IP = kVarI8Pack;
+    constexpr unsigned PK = ab::kVarPacked, OR = kOctRestage;
     // u8 -> fp32 quantised (the headline kernel): each checked against "plain"
     std::vector<Variant> vars = {
         {"copy_linear(5B/px ceiling)", launch_copy_linear},
         {"u8->f32 tile (product)", launch_var<B | W512>},
         {"u8->f32 tile packed", launch_var<B | W512 | PK>},
-        {"u8->f32 tile st sc1 nt", launch_var<B | W512 | kVarStSc1>},
-        {"u8->f32 tile st sc1", launch_var<(B & ~N) | W512 | kVarStSc1>},
-        {"u8->f32 tile st sc0sc1 nt", launch_var<B | W512 | kVarStSc0Sc1>},
-        {"u8->f32 tile st sc0sc1", launch_var<(B & ~N) | W512 | kVarStSc0Sc1>},
+        {"u8->f32 tile st sc1 nt", launch_var<B | W512 | ab::kVarStSc1>},
+        {"u8->f32 tile st sc1", launch_var<(B & ~N) | W512 | ab::kVarStSc1>},
+        {"u8->f32 tile st sc0sc1 nt", launch_var<B | W512 | ab::kVarStSc0Sc1>},
+        {"u8->f32 tile st sc0sc1", launch_var<(B & ~N) | W512 | ab::kVarStSc0Sc1>},
         {"u8->f32 tile plain st", launch_var<(B & ~N) | W512>},
         {"u8->f32 octet", launch_fwd_oct<uint8_t, float, F | N | OR>},
-        {"u8->f32 tile xcd-swz", launch_var<B | W512 | kVarXcdSwz>},
+        {"u8->f32 tile xcd-swz", launch_var<B | W512 | ab::kVarXcdSwz>},
         {"u8->f32 tile (product)", launch_var<B | W512>},
     };
     // pairs (2k, 2k+1), checked bit-exact against each other
@@ -400,11 +401,11 @@ int main(int argc, char** argv) {
         {"pattern copy u8->i8 (no math)", launch_pattern_copy},
         {"pattern copy u8->i8 (no math)", launch_pattern_copy},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
-        {"fwd u8->i8 two sets", launch_i8_two<F | N | W512 | IP | kVarTwoSets>},
+        {"fwd u8->i8 two sets", launch_i8_two<F | N | W512 | IP | ab::kVarTwoSets>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
-        {"fwd u8->i8 two sets b256", launch_i8_two<F | N | IP | kVarTwoSets>},
+        {"fwd u8->i8 two sets b256", launch_i8_two<F | N | IP | ab::kVarTwoSets>},
         {"u8->f32 tile", launch_fwd_any<uint8_t, float, B | W512>},
-        {"u8->f32 two sets", launch_f32_two<B | W512 | kVarTwoSets>},
+        {"u8->f32 two sets", launch_f32_two<B | W512 | ab::kVarTwoSets>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
         {"fwd u8->i8 tile packed", launch_fwd_any<uint8_t, int8_t, F | N | W512 | PK>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
@@ -412,9 +413,9 @@ int main(int argc, char** argv) {
         {"inv i8->u8 tile", launch_inv_any<int8_t, uint8_t, N | W512>},
         {"inv i8->u8 octet", launch_inv_oct<int8_t, uint8_t, N>},
         {"fwd u8->i8 tile", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP>},
-        {"fwd u8->i8 tile xcd-swz", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP | kVarXcdSwz>},
+        {"fwd u8->i8 tile xcd-swz", launch_fwd_any<uint8_t, int8_t, F | N | W512 | IP | ab::kVarXcdSwz>},
         {"inv i8->u8 tile", launch_inv_any<int8_t, uint8_t, N | W512>},
-        {"inv i8->u8 tile xcd-swz", launch_inv_any<int8_t, uint8_t, N | W512 | kVarXcdSwz>},
+        {"inv i8->u8 tile xcd-swz", launch_inv_any<int8_t, uint8_t, N | W512 | ab::kVarXcdSwz>},
     };
     // correctness: every DCT variant equal to "plain" bit for bit
     std::vector<float> ref(px), got(px);

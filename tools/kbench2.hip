@@ -12,18 +12,24 @@
 //   rt    uint8 frame -> fp32 coefficients + reconstruction (+ PEEN/MSE sums):
 //         the two product kernels against the one-pass round trip
 //
-//   kbench2 [n=8192] [iters=64] [rounds=3] [group=all|inv|i8|rt]
+//   wide  uint8 -> fp32 (the headline kernel) on wide / large / short frames:
+//         workgroup sizes, NT loads, column panels, two sets per wave,
+//         persistent waves with prefetch
+//
+//   kbench2 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|inv|i8|rt|wide] [sets=4] [alloc=0|1]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <string>
 #include <vector>
 
 #include "hpdct_launch.hpp"
+#include "kbench_variants.hpp"
 #include "hpdct_roundtrip.hpp"
 
 using namespace hpdct;
@@ -57,7 +63,7 @@ struct Variant {
 // ---- inverse fp32 -> u8 ----------------------------------------------------
 template <unsigned kVar>
 void inv_tile(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    hipLaunchKernelGGL((idct_kernel<float, uint8_t, true, true, kVar>), grid_for(c.g, false, c.cus, kBlock<kVar>),
+    hipLaunchKernelGGL((ab::idct_kernel<float, uint8_t, true, true, kVar>), grid_for(c.g, false, c.cus, kBlock<kVar>),
                        dim3(kBlock<kVar>), 0, s, static_cast<const float*>(in), static_cast<uint8_t*>(out), nullptr,
                        c.g, nullptr, c.qp.q, 128.0f);
 }
@@ -77,7 +83,7 @@ void inv_duo(const void* in, void* out, const Ctx& c, hipStream_t s) {
 // ---- forward u8 -> int8 ----------------------------------------------------
 template <unsigned kVar, uint32_t kLdsBytes = 0>
 void i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), kLdsBytes, s,
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp,
                        128.0f);
@@ -86,10 +92,26 @@ void i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
 // ---- forward u8 -> fp32 (the headline kernel), set order A/B on wide frames
 template <unsigned kVar>
 void f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kVar>),
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp,
                        128.0f);
+}
+
+// two sets per wave (all 16 row loads up front) and persistent waves with a
+// prefetch of the next set: half the grid / a resident grid
+template <unsigned kVar>
+void f32_fwd_two(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t sets = (c.g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar | ab::kVarTwoSets>),
+                       dim3(((sets + 1) / 2 + per - 1) / per), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+template <unsigned kVar>
+void f32_fwd_persist(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar | ab::kVarPersist2>),
+                       grid_for(c.g, true, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
 }
 
 // ---- round trip u8 -> fp32 coefficients + reconstruction (+ sums) ---------
@@ -104,7 +126,7 @@ int set_of(const void* in) {
 }
 void rt_two_kernels(const void* in, void* out, const Ctx& c, hipStream_t s) {
     float* cf = g_coef2[set_of(in)];
-    hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float> | kVarFastDiv>),
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float> | kVarFastDiv>),
                        grid_for(c.g, false, c.cus, kBlock<kProdVar<uint8_t, float>>),
                        dim3(kBlock<kProdVar<uint8_t, float>>), 0, s, static_cast<const uint8_t*>(in), cf, nullptr, c.g,
                        nullptr, c.qp, 128.0f);
@@ -125,12 +147,28 @@ void rt_raw(const void* in, void* out, const Ctx& c, hipStream_t s) {
 }
 
 int main(int argc, char** argv) {
-    const int n = argc > 1 ? atoi(argv[1]) : 8192;
+    // frame: "N" (N x N) or "HxW"
+    int n = 8192, hgt = 8192;
+    if (argc > 1) {
+        n = hgt = atoi(argv[1]);
+        if (const char* x = strchr(argv[1], 'x')) n = atoi(x + 1);
+    }
     const int iters = argc > 2 ? atoi(argv[2]) : 64;
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;
     const std::string only = argc > 4 ? argv[4] : "all";
-    const int nsets = 4;
-    const size_t px = (size_t)n * n;
+    const int nsets = argc > 5 ? atoi(argv[5]) : 4;  // rotating buffer sets (>= 3: the checks use sets 1..3)
+    // device allocation: 0 hipMalloc per buffer, 1 hipExtMallocWithFlags(hipDeviceMallocContiguous)
+    const int amode = argc > 6 ? atoi(argv[6]) : 0;
+    auto dalloc = [&](auto** p, size_t bytes) {
+        void* v = nullptr;
+        if (amode == 1) {
+            CK(hipExtMallocWithFlags(&v, bytes, hipDeviceMallocContiguous));
+        } else {
+            CK(hipMalloc(&v, bytes));
+        }
+        *p = static_cast<std::remove_pointer_t<decltype(p)>>(v);
+    };
+    const size_t px = (size_t)hgt * n;
     Ctx c;
     c.g = TileGrid{(uint32_t)(px / 64), (uint32_t)(n / 8), (uint64_t)n};
     for (int i = 0; i < 64; ++i) {
@@ -150,13 +188,13 @@ int main(int argc, char** argv) {
     srand(42);
     for (size_t i = 0; i < px; ++i) h[i] = (uint8_t)(rand() % 256);
     for (int s = 0; s < nsets; ++s) {
-        CK(hipMalloc(&img[s], px));
-        CK(hipMalloc(&coef[s], px * 4));
-        CK(hipMalloc(&out[s], px * 4));
+        dalloc(&img[s], px);
+        dalloc(&coef[s], px * 4);
+        dalloc(&out[s], px * 4);
         std::vector<uint8_t> hs(px);
         for (size_t i = 0; i < px; ++i) hs[i] = h[(i * 7919u + 13u * s) % px];
         CK(hipMemcpy(img[s], hs.data(), px, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL((fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float>>),
+        hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float>>),
                            grid_for(c.g, false, c.cus, kBlock<kProdVar<uint8_t, float>>),
                            dim3(kBlock<kProdVar<uint8_t, float>>), 0, 0, img[s], coef[s], nullptr, c.g, nullptr, c.qp,
                            128.0f);
@@ -164,11 +202,11 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     g_img = img;
     g_coef2.resize(nsets);
-    for (int s = 0; s < nsets; ++s) CK(hipMalloc(&g_coef2[s], px * 4));
+    for (int s = 0; s < nsets; ++s) dalloc(&g_coef2[s], px * 4);
     CK(hipMalloc(&g_sums, sizeof(RtSums)));
 
-    constexpr unsigned N = kVarNT, W512 = 2u << 12, W1024 = 3u << 12, LL = kVarLdsLoad, OR = kOctRestage;
-    constexpr unsigned F = kVarFastDiv, IP = kVarI8Pack, PR = kVarPrio;
+    constexpr unsigned N = kVarNT, W512 = 2u << 12, W1024 = 3u << 12, LL = ab::kVarLdsLoad, OR = kOctRestage;
+    constexpr unsigned F = kVarFastDiv, IP = kVarI8Pack, PR = ab::kVarPrio;
     constexpr unsigned I8 = F | N | W512 | IP;  // the product's int8 forward
     std::vector<Variant> vars = {
         {"inv", "inv f32->u8 tile (product)", inv_tile<kProdVar<float, uint8_t>>, true},
@@ -195,14 +233,17 @@ int main(int argc, char** argv) {
         {"rt", "rt fused f32 recon + sums (9 B/px)", rt_fused<kRtReconF32, true, true>, false},
         {"rt", "rt fused u8 recon + sums, IEEE/fp32 q", rt_fused<kRtReconU8, true, false>, true},
         {"wide", "fwd u8->f32 tile (product)", f32_fwd<kProdVar<uint8_t, float> | F>, true},
-        {"wide", "fwd u8->f32 tile panel 4096 px", f32_fwd<kProdVar<uint8_t, float> | F | kVarPanel>, true},
-        {"wide", "fwd u8->f32 tile nt loads", f32_fwd<kProdVar<uint8_t, float> | F | kVarNTLoad>, true},
+        {"wide", "fwd u8->f32 tile panel 4096 px", f32_fwd<kProdVar<uint8_t, float> | F | ab::kVarPanel>, true},
+        {"wide", "fwd u8->f32 tile nt loads", f32_fwd<kProdVar<uint8_t, float> | F | ab::kVarNTLoad>, true},
         {"wide", "fwd u8->f32 tile b256", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | F>, true},
         {"wide", "fwd u8->f32 tile b1024", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | W1024 | F>, true},
+        {"wide", "fwd u8->f32 tile two sets/wave", f32_fwd_two<kProdVar<uint8_t, float> | F>, true},
+        {"wide", "fwd u8->f32 tile two sets/wave b256", f32_fwd_two<(kProdVar<uint8_t, float> & ~(3u << 12)) | F>, true},
+        {"wide", "fwd u8->f32 tile persistent+prefetch", f32_fwd_persist<kProdVar<uint8_t, float> | F>, true},
         {"wide", "fwd u8->f32 tile (product) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
-        {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | kVarNoLoad>, false},
-        {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | kVarNoStore>, false},
-        {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | kVarNoLoad | kVarNoStore>, false},
+        {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | ab::kVarNoLoad>, false},
+        {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | ab::kVarNoStore>, false},
+        {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | ab::kVarNoLoad | ab::kVarNoStore>, false},
     };
     vars.erase(std::remove_if(vars.begin(), vars.end(),
                               [&](const Variant& v) { return only != "all" && v.group != only; }),

@@ -33,6 +33,11 @@ def main():
         # common video widths (not multiples of 512 px) against power-of-2 neighbours
         shapes = [(32768, 1024), (32768, 1280), (16384, 1920), (16384, 2048), (8192, 3840), (8192, 4096),
                   (4320, 7680), (4096, 8192)]
+    steps = 80
+    if len(sys.argv) > 1 and sys.argv[1] == "pmc":
+        # short runs for counter passes (tools/pmc_limits.sh): one shape per row stride
+        shapes = [(8192, 8192), (16384, 4096), (4096, 16384), (2048, 16384), (16384, 16384)]
+        steps = 16
     if len(sys.argv) > 1 and sys.argv[1] == "ab":
         shapes = [(8192, 8192), (2048, 16384), (16384, 1920), (32768, 1280), (8192, 8200)]
     if len(sys.argv) > 1 and sys.argv[1] == "f32":
@@ -66,7 +71,7 @@ def main():
         for s, t in enumerate(ins):
             hpdct.fill_hash_u8(t, seed=s)
         outs = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in range(sets)]
-        us = us_per_launch([hpdct.bind("fwd", ins[s], outs[s]) for s in range(sets)])
+        us = us_per_launch([hpdct.bind("fwd", ins[s], outs[s]) for s in range(sets)], steps=steps)
         px = h * w
         print(f"{h:6d} x {w:6d}  {us:9.2f} us  {us * 64 * 2**20 / px:8.2f} us per 64 Mpx  "
               f"{5 * px / us / 1e6:7.3f} TB/s", flush=True)
