@@ -14,8 +14,11 @@ waits for all of them and exits non-zero if any fails.
 A step = one launch of the fused gfx950 forward kernel over one 8192x8192
 frame already resident in HBM (uint8 pixels in, fp32 quantised coefficients
 out, reference layout; 5 algorithmic bytes per pixel).  Frames rotate over
-buffer sets totalling > 1 GB per GPU so the 256 MiB Infinity Cache cannot
-serve them.  Weak scaling: every rank processes its own frame per step (the
+enough buffer sets that the INPUT planes alone total >= 4x the 256 MiB
+Infinity Cache (16 sets at 8192^2): non-temporal output stores do not
+allocate there, so with fewer sets (4 x 64 MiB inputs fit it exactly) the
+reads would be served from the cache, not HBM (tools/kbench2 set sweep,
+profiles/r02/kbench2_sets_r02.log).  Weak scaling: every rank processes its own frame per step (the
 frames are independent), no collective in the timed region; value = pixels
 of all ranks / max-over-ranks time.
 
@@ -45,6 +48,15 @@ T4_FWD_8192_MS = 14.70         # README.md:55, T4
 BYTES_PER_PX = {"u8_f32": 5, "f32_f32": 8, "u8_i8": 2, "inv_f32_f32": 8}
 EXTRA_STEPS = 100              # timed launches per extra (independent of --steps)
 EXTRA_WARM_S = 0.02            # untimed steady-state lead-in per extra (>= 20 ms)
+MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MI355X_MICROARCH.md)
+INPUT_FOOTPRINT = 4 * MALL_BYTES  # rotating inputs must total at least this
+
+
+def sets_for(input_bytes: int, minimum: int = 2) -> int:
+    """Rotating buffer sets so that the inputs of all sets total
+    >= INPUT_FOOTPRINT: every launch then reads its input from HBM, not from
+    the Infinity Cache (which the output stores, non-temporal, do not fill)."""
+    return max(minimum, -(-INPUT_FOOTPRINT // max(1, input_bytes)))
 
 
 def parse():
@@ -53,7 +65,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=8192, help="square frame side (C3: 8192)")
-    ap.add_argument("--sets", type=int, default=4, help="rotating buffer sets per GPU")
+    ap.add_argument("--sets", type=int, default=None,
+                    help="rotating buffer sets per GPU (default: inputs total >= 4x the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--c4-size", type=int, default=16384)
@@ -147,6 +160,8 @@ def main():
     hpdct.load_library()
     n = args.size
     px = n * n
+    if args.sets is None:
+        args.sets = sets_for(px, minimum=4)
     stream = torch.cuda.current_stream()
 
     # ---- inputs resident in HBM: set 0 = the reference's benchmark frame
@@ -235,7 +250,8 @@ def main():
         "vs_baseline": round(value / (px / (T4_FWD_8192_MS * 1e-3) / 1e9), 2) if n == 8192 else None,
         "dtype": "f32",
         "data": "synthetic: set0 = srand(42) rand()%256 (benchmark_newAppr.cu:46-51), sets1.. device hash; "
-                f"{args.sets} rotating buffer sets ({args.sets * 5 * px / 2**30:.2f} GiB/GPU)",
+                f"{args.sets} rotating buffer sets ({args.sets * 5 * px / 2**30:.2f} GiB/GPU; inputs "
+                f"{args.sets * px / 2**30:.2f} GiB = {args.sets * px / MALL_BYTES:.1f}x the Infinity Cache)",
         "config": {
             "workload": f"C3: {n}x{n} uint8 frame -> fp32 quantised 8x8 DCT coefficients (HpApprDCT, "
                         "standard JPEG Q), one fused kernel launch per frame",
@@ -405,17 +421,19 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         # single-frame launch is dominated by the per-dispatch cost (~4 us; a
         # HIP graph of the same launches does not remove it,
         # profiles/r01/c2_probe.log).  32 frames stacked as one (32*1024) x 1024
-        # image (the C-ABI's batch layout) make one launch; 2 sets of 160 MB
+        # image (the C-ABI's batch layout) make one launch; 32 MiB of input per
+        # launch, rotated over sets_for() sets (1 GiB of inputs)
         nb = 32
-        c2b_in = [torch.empty((nb * c2, c2), dtype=torch.uint8, device=dev) for _ in range(2)]
+        nbs = sets_for(nb * c2 * c2)
+        c2b_in = [torch.empty((nb * c2, c2), dtype=torch.uint8, device=dev) for _ in range(nbs)]
         for s, t in enumerate(c2b_in):
             hpdct.fill_hash_u8(t, seed=4242 + s)
-        c2b_out = [torch.empty((nb * c2, c2), dtype=torch.float32, device=dev) for _ in range(2)]
-        calls = [hpdct.bind("fwd", c2b_in[s], c2b_out[s], stream=stream) for s in range(2)]
+        c2b_out = [torch.empty((nb * c2, c2), dtype=torch.float32, device=dev) for _ in range(nbs)]
+        calls = [hpdct.bind("fwd", c2b_in[s], c2b_out[s], stream=stream) for s in range(nbs)]
         rms, k, _ = timed_loop(calls, steps, 5)
         line = _line(nb * c2 * c2, rms / steps, float(k.mean()), BYTES_PER_PX["u8_f32"], world)
         line["us_per_frame"] = round(rms / steps / nb * 1e3, 3)
-        line["note"] = f"{nb} 1024^2 frames per launch, stacked (C-ABI batch layout)"
+        line["note"] = f"{nb} 1024^2 frames per launch, stacked (C-ABI batch layout), {nbs} rotating sets"
         extras["c2_batched_fwd_u8_f32"] = line
         del c2b_in, c2b_out
         torch.cuda.empty_cache()
@@ -508,18 +526,19 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     from hpdct_dist import gather_slabs, shard_rows
     n = args.c4_size
     r0, rows = shard_rows(n, world, rank)
-    # two identical buffer sets, alternated: at 8 ranks one slab set (32 MiB in
-    # + 128 MiB out) would otherwise stay resident in the 256 MiB Infinity Cache
-    xs = [torch.empty((rows, n), dtype=torch.uint8, device=dev) for _ in range(2)]
+    # identical slab buffer sets, rotated: their inputs total >= 4x the
+    # Infinity Cache (at 8 ranks a slab reads 32 MiB: 32 sets)
+    nsl = sets_for(rows * n)
+    xs = [torch.empty((rows, n), dtype=torch.uint8, device=dev) for _ in range(nsl)]
     for t in xs:
         hpdct.fill_hash_u8(t, seed=42, first_index=r0 * n)
-    ys = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(2)]
+    ys = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(nsl)]
     x, y = xs[0], ys[0]
-    calls = [hpdct.bind("fwd", xs[i], ys[i], stream=stream) for i in range(2)]
+    calls = [hpdct.bind("fwd", xs[i], ys[i], stream=stream) for i in range(nsl)]
     reps = EXTRA_STEPS
     rms, _, _ = timed_loop(calls, reps, 4)
     compute_ms = max_over_ranks(rms / reps)
-    out = {"frame": [n, n], "rows_per_rank": rows, "compute_ms_max_rank": round(compute_ms, 4),
+    out = {"frame": [n, n], "rows_per_rank": rows, "slab_sets": nsl, "compute_ms_max_rank": round(compute_ms, 4),
            "compute_gpx_s": round(n * n / (compute_ms * 1e-3) / 1e9, 2),
            "compute_hbm_frac_max_rank": round(5 * rows * n / (compute_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if world > 1:
@@ -560,15 +579,15 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
             ref = hpdct.forward(xf)
             out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
             # the same full frame on this one GPU: the compute-phase node speedup
-            # (BASELINE.md C4 target >= 6x at 8 GPUs); two sets alternated as above
+            # (BASELINE.md C4 target >= 6x at 8 GPUs); sets rotated as above
             del full
-            xf2 = xf.clone()
-            ref2 = torch.empty_like(ref)
-            fcalls = [hpdct.bind("fwd", xf, ref, stream=stream), hpdct.bind("fwd", xf2, ref2, stream=stream)]
+            xfs = [xf] + [xf.clone() for _ in range(sets_for(n * n) - 1)]
+            refs = [ref] + [torch.empty_like(ref) for _ in range(len(xfs) - 1)]
+            fcalls = [hpdct.bind("fwd", a, b, stream=stream) for a, b in zip(xfs, refs)]
             one_gpu_ms = _steady_ms(torch, fcalls, reps, stream)
             out["one_gpu_full_frame_ms"] = round(one_gpu_ms, 4)
             out["compute_speedup_vs_1gpu"] = round(one_gpu_ms / compute_ms, 2)
-            del xf, ref, xf2, ref2
+            del xf, ref, xfs, refs
         barrier()
     del x, y, xs, ys
     torch.cuda.empty_cache()

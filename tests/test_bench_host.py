@@ -35,9 +35,23 @@ def test_cpu_baseline_block_small_frame():
 def test_defaults_are_the_driver_contract(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     args = bench.parse()
-    assert args.gpus == 1 and args.size == 8192 and args.sets >= 3
+    assert args.gpus == 1 and args.size == 8192 and args.sets is None  # derived from the frame size
     assert args.steps > 0 and args.warmup > 0 and args.backend == "nccl"
     assert bench.BYTES_PER_PX["u8_f32"] == 5 and bench.HBM_PEAK_GBS == 8000.0
+
+
+def test_rotating_sets_keep_inputs_out_of_the_infinity_cache():
+    """Inputs of all rotating sets total >= 4x the 256 MiB Infinity Cache, so
+    every timed launch reads HBM (4 sets of 64 MiB u8 frames fit the cache:
+    profiles/r02/kbench2_sets_r02.log, 50 vs 61 us)."""
+    mall = 256 << 20
+    assert bench.MALL_BYTES == mall
+    for in_bytes in (8192 * 8192, 16384 * 16384, 2048 * 16384, 32 << 20, 1 << 30):
+        k = bench.sets_for(in_bytes)
+        assert k * in_bytes >= 4 * mall and k >= 2
+    assert bench.sets_for(8192 * 8192, minimum=4) == 16
+    assert bench.sets_for(16384 * 16384) == 4
+    assert bench.sets_for(2048 * 16384) == 32
 
 
 def test_gpus_n_self_launches_ranks_without_torch(tmp_path):

@@ -16,7 +16,7 @@
 //         workgroup sizes, NT loads, column panels, two sets per wave,
 //         persistent waves with prefetch
 //
-//   kbench2 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|inv|i8|rt|wide] [sets=4] [alloc=0|1]
+//   kbench2 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|inv|i8|rt|wide|tlb|tlb8] [sets=4] [alloc=0|1]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -90,10 +90,10 @@ void i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
 }
 
 // ---- forward u8 -> fp32 (the headline kernel), set order A/B on wide frames
-template <unsigned kVar>
+template <unsigned kVar, uint32_t kLdsBytes = 0>
 void f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar>),
-                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), kLdsBytes, s,
                        static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp,
                        128.0f);
 }
@@ -112,6 +112,20 @@ void f32_fwd_persist(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, float, true, true, false, kVar | ab::kVarPersist2>),
                        grid_for(c.g, true, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+// the LIBRARY's tile kernels (hpdct_kernels_impl.hpp), for A/B of product-side variants
+template <unsigned kVar>
+void prod_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, float, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+template <unsigned kVar>
+void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
 }
 
 // ---- round trip u8 -> fp32 coefficients + reconstruction (+ sums) ---------
@@ -206,7 +220,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&g_sums, sizeof(RtSums)));
 
     constexpr unsigned N = kVarNT, W512 = 2u << 12, W1024 = 3u << 12, LL = ab::kVarLdsLoad, OR = kOctRestage;
-    constexpr unsigned F = kVarFastDiv, IP = kVarI8Pack, PR = ab::kVarPrio;
+    constexpr unsigned F = kVarFastDiv, IP = kVarI8Pack;
     constexpr unsigned I8 = F | N | W512 | IP;  // the product's int8 forward
     std::vector<Variant> vars = {
         {"inv", "inv f32->u8 tile (product)", inv_tile<kProdVar<float, uint8_t>>, true},
@@ -216,7 +230,6 @@ int main(int argc, char** argv) {
         {"inv", "inv f32->u8 duo b256", inv_duo<N>, true},
         {"inv", "inv f32->u8 duo b512 plain st", inv_duo<W512>, true},
         {"i8", "fwd u8->i8 (product)", i8_fwd<I8>, true},
-        {"i8", "fwd u8->i8 prio", i8_fwd<I8 | PR>, true},
         {"i8", "fwd u8->i8 b256", i8_fwd<F | N | IP>, true},
         {"i8", "fwd u8->i8 b1024", i8_fwd<F | N | IP | W1024>, true},
         {"i8", "fwd u8->i8 lds 1 wg/cu (2 w/simd)", i8_fwd<I8, 84 * 1024>, true},
@@ -237,10 +250,20 @@ int main(int argc, char** argv) {
         {"wide", "fwd u8->f32 tile nt loads", f32_fwd<kProdVar<uint8_t, float> | F | ab::kVarNTLoad>, true},
         {"wide", "fwd u8->f32 tile b256", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | F>, true},
         {"wide", "fwd u8->f32 tile b1024", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | W1024 | F>, true},
+        {"wide", "fwd u8->f32 tile lds 1 wg/cu (2 w/simd)", f32_fwd<kProdVar<uint8_t, float> | F, 100 * 1024>, true},
+        {"wide", "fwd u8->f32 tile lds 2 wg/cu (4 w/simd)", f32_fwd<kProdVar<uint8_t, float> | F, 60 * 1024>, true},
+        {"wide", "fwd u8->f32 tile lds 3 wg/cu (6 w/simd)", f32_fwd<kProdVar<uint8_t, float> | F, 36 * 1024>, true},
+        {"wide", "fwd u8->f32 tile b256 lds 2 wg/cu (2 w/simd)", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | F, 60 * 1024>, true},
+        {"wide", "fwd u8->f32 tile b256 lds 3 wg/cu (3 w/simd)", f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | F, 40 * 1024>, true},
         {"wide", "fwd u8->f32 tile two sets/wave", f32_fwd_two<kProdVar<uint8_t, float> | F>, true},
         {"wide", "fwd u8->f32 tile two sets/wave b256", f32_fwd_two<(kProdVar<uint8_t, float> & ~(3u << 12)) | F>, true},
         {"wide", "fwd u8->f32 tile persistent+prefetch", f32_fwd_persist<kProdVar<uint8_t, float> | F>, true},
         {"wide", "fwd u8->f32 tile (product) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"tlb", "fwd u8->f32 library kernel", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"tlb", "fwd u8->f32 library + translation touch", prod_f32_fwd<kProdVar<uint8_t, float> | F | kVarTlbTouch>, true},
+        {"tlb", "fwd u8->f32 library kernel again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"tlb8", "fwd u8->i8 library kernel", prod_i8_fwd<I8>, true},
+        {"tlb8", "fwd u8->i8 library + translation touch", prod_i8_fwd<I8 | kVarTlbTouch>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | ab::kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | ab::kVarNoStore>, false},
         {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | ab::kVarNoLoad | ab::kVarNoStore>, false},
@@ -256,7 +279,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> ref(px * 4), got(px * 4);
         std::string cur;
         for (auto& v : vars) {
-            const size_t nb = v.group == "wide" ? px * 4 : px;  // fp32 output plane
+            const size_t nb = v.group == "wide" || v.group == "tlb" ? px * 4 : px;  // fp32 output plane
             CK(hipMemset(out[2], 0xa5, nb));
             v.launch(src(v, 1), out[2], c, 0);
             const hipError_t le = hipGetLastError();
@@ -343,7 +366,7 @@ int main(int argc, char** argv) {
         if (t.empty()) continue;
         std::sort(t.begin(), t.end());
         const double med = t[t.size() / 2];
-        double bpp = vars[v].group == "inv" || vars[v].group == "wide" ? 5.0 : 2.0;
+        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" ? 5.0 : 2.0;
         if (vars[v].group == "rt") {
             const std::string& nm = vars[v].name;
             bpp = nm.find("(10 B") != std::string::npos  ? 10.0

@@ -14,7 +14,6 @@
 //   kVarStSc1 / kVarStSc0Sc1    store cache policies
 //   kVarPacked                  packed-fp32 (v_pk_fma_f32) transform
 //   kVarFiniteSkip              zero-term skip for finite fp32 tiles
-//   kVarPrio                    s_setprio around the load phase
 //   kVarXcdSwz / kVarPanel      XCD-contiguous / column-panel set orders
 //   bits 8..11                  minimum waves per SIMD for the register allocator
 //   kVarNoLoad / kVarNoStore    diagnostics: phase split of the kernel time
@@ -59,7 +58,7 @@ enum : unsigned {
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
                                 // all finite -> the zero terms of T are skipped (exact: a chain from +0
                                 // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
-    kVarPrio = 1u << 26,        // s_setprio 3 while the wave computes its addresses and issues its loads
+    // (1u << 26 is the library's kVarTlbTouch)
     // diagnostics only (tools/kbench): split the kernel's time into its phases
     kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
     kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
@@ -568,7 +567,6 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         }
     } else if constexpr (!kPersist) {
         if (wave >= nsets) return;
-        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(3);
         TilePos p;
         uint64_t seg;
         uint32_t ok;
@@ -604,7 +602,6 @@ __device__ __forceinline__ void walk_sets(const TIn* __restrict__ src, const Til
         } else {
             raw.load(src + p.base, g.width);
         }
-        if constexpr ((kVar & kVarPrio) != 0) __builtin_amdgcn_s_setprio(0);
         body(raw, p, ok, seg);
     } else {
         const uint32_t nwaves = gridDim.x * (kBlock<kVar> / 64u);

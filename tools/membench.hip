@@ -2,7 +2,8 @@
 // the DCT kernels on MI355X: pure read, pure write, and the 1-B-in / 4-B-out
 // streaming mix of the uint8 -> fp32 forward pass, with plain and
 // non-temporal stores, several per-lane widths and grid sizes.  Buffers
-// rotate over > 1 GB so the 256 MiB Infinity Cache does not serve them.
+// rotate over 16 sets (1 GiB of u8 inputs) so the 256 MiB Infinity Cache does
+// not serve the reads.  usage: membench [n=8192] [iters=40] [all|u8|f32] [sets=16]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -72,6 +73,32 @@ __global__ __launch_bounds__(256) void mix_w16(const uint4* __restrict__ in, flo
             st4<kNT>(&out[c * 256u + p], cvt4(v));
         }
     }
+}
+
+// 1 B in -> 4 B out, each wave one contiguous run of kRun pixels (kRun/256
+// store instructions of 1 KiB), no grid-stride interleaving between waves
+template <uint32_t kRun>
+__global__ __launch_bounds__(256) void mix_run(const uint32_t* __restrict__ in, float4* __restrict__ out, uint64_t n4) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i0 = wave * (kRun / 4);
+    if (i0 >= n4) return;
+    uint32_t w[kRun / 256];
+#pragma unroll
+    for (uint32_t k = 0; k < kRun / 256; ++k) w[k] = in[i0 + 64u * k + lane];
+#pragma unroll
+    for (uint32_t k = 0; k < kRun / 256; ++k) st4<true>(&out[i0 + 64u * k + lane], cvt4(w[k]));
+}
+
+// write-only, each wave one contiguous run of kRun floats
+template <uint32_t kRun>
+__global__ __launch_bounds__(256) void write_run(float4* __restrict__ out, uint64_t n4) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i0 = wave * (kRun / 4);
+    if (i0 >= n4) return;
+#pragma unroll
+    for (uint32_t k = 0; k < kRun / 256; ++k) st4<true>(&out[i0 + 64u * k + lane], make_float4(1.f, 2.f, 3.f, 4.f));
 }
 
 // fp32 -> fp32 (4 B in + 4 B out per px), 16 B per lane each way, grid-stride
@@ -200,7 +227,10 @@ int main(int argc, char** argv) {
     }
     const int n = argc > 1 ? atoi(argv[1]) : 8192;
     const int iters = argc > 2 ? atoi(argv[2]) : 40;
-    const int nsets = 4;
+    // rotating buffer sets: the INPUT bytes of all sets must exceed the 256 MiB
+    // Infinity Cache by a wide margin, or the reads are served from it (NT
+    // stores do not allocate there; 4 sets of 64 MiB u8 inputs fit exactly).
+    const int nsets = argc > 4 ? atoi(argv[4]) : 16;
     const size_t px = (size_t)n * n;
     int dev = 0, cus = 0;
     CK(hipGetDevice(&dev));
@@ -221,7 +251,7 @@ int main(int argc, char** argv) {
     };
     std::vector<Case> cases;
     const uint64_t n4 = px / 4, n16 = px / 16;
-    for (int gm : {4, 8, 16, 32}) {
+    for (int gm : {1, 2, 4, 8, 16, 32}) {
         const unsigned grid = cus * gm;
         cases.push_back({"mix_w4 plain g" + std::to_string(gm), 5.0 * px, [=](int s) {
                              hipLaunchKernelGGL(mix_w4<false>, dim3(grid), dim3(256), 0, 0,
@@ -254,6 +284,26 @@ int main(int argc, char** argv) {
                                                 (const float4*)out[(s + 1) % nsets], (float4*)out[s], n4);
                          }});
     }
+    cases.push_back({"mix_run 4096 px/wave nt", 5.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(mix_run<4096>, dim3((unsigned)(px / 4096 / 4)), dim3(256), 0, 0,
+                                            (const uint32_t*)in[s], (float4*)out[s], n4);
+                     }});
+    cases.push_back({"mix_run 1024 px/wave nt", 5.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(mix_run<1024>, dim3((unsigned)(px / 1024 / 4)), dim3(256), 0, 0,
+                                            (const uint32_t*)in[s], (float4*)out[s], n4);
+                     }});
+    cases.push_back({"mix_run 16384 px/wave nt", 5.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(mix_run<16384>, dim3((unsigned)(px / 16384 / 4)), dim3(256), 0, 0,
+                                            (const uint32_t*)in[s], (float4*)out[s], n4);
+                     }});
+    cases.push_back({"write_run 4096/wave nt", 4.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(write_run<4096>, dim3((unsigned)(px / 4096 / 4)), dim3(256), 0, 0,
+                                            (float4*)out[s], n4);
+                     }});
+    cases.push_back({"write_run 16384/wave nt", 4.0 * px, [=](int s) {
+                         hipLaunchKernelGGL(write_run<16384>, dim3((unsigned)(px / 16384 / 4)), dim3(256), 0, 0,
+                                            (float4*)out[s], n4);
+                     }});
     const uint32_t ntiles = px / 64, tiles_x = n / 8;
     cases.push_back({"tile_mix plain", 5.0 * px, [=](int s) {
                          hipLaunchKernelGGL(tile_mix<false>, dim3((ntiles + 255) / 256), dim3(256), 0, 0, in[s],
@@ -263,7 +313,7 @@ int main(int argc, char** argv) {
                          hipLaunchKernelGGL(tile_mix<true>, dim3((ntiles + 255) / 256), dim3(256), 0, 0, in[s],
                                             out[s], ntiles, tiles_x, (uint64_t)n);
                      }});
-    for (int gm : {8, 16}) {
+    for (int gm : {1, 2, 4, 8, 16}) {
         const unsigned grid = cus * gm;
         cases.push_back({"write_only plain g" + std::to_string(gm), 4.0 * px, [=](int s) {
                              hipLaunchKernelGGL(write_only<false>, dim3(grid), dim3(256), 0, 0, (float4*)out[s], n4);
@@ -299,6 +349,14 @@ int main(int argc, char** argv) {
                      }});
     cases.push_back({"hipMemsetD32 4B/px", 4.0 * px, [=](int s) { CK(hipMemsetD32Async((hipDeviceptr_t)out[s], 7, px, 0)); }});
 
+    if (argc > 3 && strcmp(argv[3], "mix") == 0) {
+        std::vector<Case> keep;
+        for (auto& c : cases)
+            if (c.name.find("mix") != std::string::npos || c.name.find("write") != std::string::npos ||
+                c.name.find("Memset") != std::string::npos)
+                keep.push_back(c);
+        cases.swap(keep);
+    }
     if (argc > 3 && strcmp(argv[3], "u8") == 0) {
         std::vector<Case> keep;
         for (auto& c : cases)
@@ -321,7 +379,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < 3; ++r)
         for (size_t c = 0; c < cases.size(); ++c) {
             for (int w = 0; w < 3; ++w) cases[c].run(w % nsets);
-            for (int i = 0; i < iters; ++i) {
+            for (int i = 3; i < iters + 3; ++i) {  // sets not touched by the warm-up first
                 CK(hipEventRecord(a, 0));
                 cases[c].run(i % nsets);
                 CK(hipEventRecord(b, 0));
