@@ -39,10 +39,6 @@ enum : unsigned {
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
-    kVarTlbTouch = 1u << 26,  // every 16th wave touches the input and output planes kTouchAhead bytes past its
-                              // own set with a scalar load, so the address translations of the pages the
-                              // leading waves are about to reach are walked before they get there (frames and
-                              // buffer rotations whose footprint exceeds the translation caches' reach)
     kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
                               // multiple of 512 px) stores two contiguous runs per instruction instead of
                               // 32 B per lane; launched only for such widths (the branch costs the
@@ -431,39 +427,6 @@ __device__ __forceinline__ bool wave_tame(const float (&x)[8][8]) {
     return __builtin_amdgcn_ballot_w64(m >= 0x7e000000u) == 0;
 }
 
-// Translation touch (kVarTlbTouch): a scalar load of one dword, kTouchAhead
-// bytes (output plane; input plane in proportion) past the wave's own set,
-// clamped into the plane.  The loaded value is never used: keep_touch() at the
-// kernel's end holds the destination SGPRs until the loads have landed (the
-// compiler does not count inline-asm loads in its waits).
-constexpr uint64_t kTouchAhead = 16ull << 20;
-constexpr uint32_t kTouchEvery = 16;  // waves
-struct Touch {
-    uint32_t a = 0, b = 0;
-};
-__device__ __forceinline__ uint32_t touch_dword(const void* plane, uint64_t off, uint64_t bytes) {
-    if (off + 4 > bytes) off = bytes - 4;
-    const uint64_t addr = (reinterpret_cast<uint64_t>(plane) + off) & ~static_cast<uint64_t>(3);
-    uint32_t v;
-    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(addr));
-    return v;
-}
-template <typename TIn, typename TOut>
-__device__ __forceinline__ Touch touch_ahead(const TIn* img, const TOut* out, const TileGrid& g, uint32_t wave) {
-    Touch t;
-    if ((wave % kTouchEvery) != 0) return t;
-    const uint32_t t0 = wave * 64u;
-    const uint32_t ty0 = t0 / g.tiles_x, tx0 = t0 - ty0 * g.tiles_x;
-    const uint64_t e = static_cast<uint64_t>(ty0) * 8u * g.width + static_cast<uint64_t>(tx0) * 8u;
-    const uint64_t px = static_cast<uint64_t>(g.ntiles) * 64u;
-    t.a = touch_dword(out, e * sizeof(TOut) + kTouchAhead, px * sizeof(TOut));
-    t.b = touch_dword(img, e * sizeof(TIn) + kTouchAhead * sizeof(TIn) / sizeof(TOut), px * sizeof(TIn));
-    return t;
-}
-__device__ __forceinline__ void keep_touch(const Touch& t) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(t.a), "s"(t.b));
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -479,11 +442,6 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __rest
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     const RowSink<kVar, float> wb_sink{shifted, g.width, slots};
-    Touch touch;
-    if constexpr ((kVar & kVarTlbTouch) != 0) {
-        touch = touch_ahead(img, out, g,
-                            __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u));
-    }
 
     walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         float x[8][8];
@@ -510,7 +468,6 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __rest
             fdct_tile(T, x, emit);
         }
     });
-    if constexpr ((kVar & kVarTlbTouch) != 0) keep_touch(touch);
 }
 
 // ---------------------------------------------------------------------------

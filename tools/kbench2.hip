@@ -260,10 +260,8 @@ int main(int argc, char** argv) {
         {"wide", "fwd u8->f32 tile persistent+prefetch", f32_fwd_persist<kProdVar<uint8_t, float> | F>, true},
         {"wide", "fwd u8->f32 tile (product) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"tlb", "fwd u8->f32 library kernel", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
-        {"tlb", "fwd u8->f32 library + translation touch", prod_f32_fwd<kProdVar<uint8_t, float> | F | kVarTlbTouch>, true},
         {"tlb", "fwd u8->f32 library kernel again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"tlb8", "fwd u8->i8 library kernel", prod_i8_fwd<I8>, true},
-        {"tlb8", "fwd u8->i8 library + translation touch", prod_i8_fwd<I8 | kVarTlbTouch>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | ab::kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | ab::kVarNoStore>, false},
         {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | ab::kVarNoLoad | ab::kVarNoStore>, false},

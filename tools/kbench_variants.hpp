@@ -58,7 +58,7 @@ enum : unsigned {
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
                                 // all finite -> the zero terms of T are skipped (exact: a chain from +0
                                 // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
-    // (1u << 26 is the library's kVarTlbTouch)
+    // (1u << 26: free; a translation-touch variant measured there in round 2 gave no gain)
     // diagnostics only (tools/kbench): split the kernel's time into its phases
     kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
     kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
