@@ -16,7 +16,7 @@
 //         workgroup sizes, NT loads, column panels, two sets per wave,
 //         persistent waves with prefetch
 //
-//   kbench2 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|inv|i8|rt|wide|tlb|tlb8] [sets=4] [alloc=0|1]
+//   kbench2 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|inv|i8|rt|wide|tlb|tlb8|mfma] [sets=4] [alloc=0|1]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -30,6 +30,7 @@
 
 #include "hpdct_launch.hpp"
 #include "kbench_variants.hpp"
+#include "kbench_mfma.hpp"
 #include "hpdct_roundtrip.hpp"
 
 using namespace hpdct;
@@ -126,6 +127,11 @@ void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+template <bool kFast>
+void mfma_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    (void)hpdct::fdct_mfma_i8_go<kFast>(static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), c.g, c.qp, s);
 }
 
 // ---- round trip u8 -> fp32 coefficients + reconstruction (+ sums) ---------
@@ -262,6 +268,10 @@ int main(int argc, char** argv) {
         {"tlb", "fwd u8->f32 library kernel", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"tlb", "fwd u8->f32 library kernel again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"tlb8", "fwd u8->i8 library kernel", prod_i8_fwd<I8>, true},
+        {"mfma", "fwd u8->i8 library tile kernel", prod_i8_fwd<I8>, true},
+        {"mfma", "fwd u8->i8 MFMA first pass", mfma_i8_fwd<true>, true},
+        {"mfma", "fwd u8->i8 MFMA first pass, IEEE quotient", mfma_i8_fwd<false>, true},
+        {"mfma", "fwd u8->i8 library tile kernel again", prod_i8_fwd<I8>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | ab::kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | ab::kVarNoStore>, false},
         {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | ab::kVarNoLoad | ab::kVarNoStore>, false},
