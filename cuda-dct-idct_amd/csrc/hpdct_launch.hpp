@@ -84,6 +84,25 @@ hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g,
     return hipGetLastError();
 }
 
+// uint8 -> fp32 tile kernels: 1024-thread workgroups for frames of at most
+// kBigWgSetsPerCU sets per CU, where the whole grid is about one round of
+// resident waves (with inputs from HBM: 2048 x 16384 35.2 -> 32.3 us,
+// 4096 x 8192 34.2 -> 31.2 us; neutral at 8192^2 (64 sets per CU), 5 % slower
+// at 16384^2; profiles/r02/kbench2_wide_hbm_r02.log, kbench2_wide_r02.log),
+// the product's 512 otherwise.
+constexpr uint32_t kBigWgSetsPerCU = 32;
+
+template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
+hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
+                        const QParams& q, float shift, hipStream_t s) {
+    if constexpr (std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float>) {
+        if ((g.ntiles + 63u) / 64u <= kBigWgSetsPerCU * device_cus())
+            return fdct_go<(kV & ~(3u << 12)) | (3u << 12), TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+                img, out, shifted, g, t_dev, q, shift, s);
+    }
+    return fdct_go<kV, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+}
+
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_octet_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                          const QParams& q, float shift, hipStream_t s) {
@@ -154,20 +173,20 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
         if (g.tiles_x % 64u != 0u) {
             if constexpr (kFastDivOk) {
                 if (fastdiv)
-                    return fdct_go<kBase | kVarFastDiv | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+                    return fdct_tile_go<kBase | kVarFastDiv | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
                         img, out, shifted, g, t_dev, q, shift, s);
             }
-            return fdct_go<kBase | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
+            return fdct_tile_go<kBase | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g,
                                                                                            t_dev, q, shift, s);
         }
     }
     if constexpr (kFastDivOk) {
         if (fastdiv)
-            return fdct_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
+            return fdct_tile_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
                                                                                           q, shift, s);
     }
     (void)fastdiv;
-    return fdct_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+    return fdct_tile_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
 }
 
 template <unsigned kV, typename TIn, typename TOut, bool kDequant, bool kBuiltinT>
