@@ -236,6 +236,7 @@ int main(int argc, char** argv) {
         {"inv", "inv f32->u8 duo b256", inv_duo<N>, true},
         {"inv", "inv f32->u8 duo b512 plain st", inv_duo<W512>, true},
         {"i8", "fwd u8->i8 (product)", i8_fwd<I8>, true},
+        {"i8", "fwd u8->i8 xor+sdwa byte convert", i8_fwd<I8 | ab::kVarXorCvt>, true},
         {"i8", "fwd u8->i8 b256", i8_fwd<F | N | IP>, true},
         {"i8", "fwd u8->i8 b1024", i8_fwd<F | N | IP | W1024>, true},
         {"i8", "fwd u8->i8 lds 1 wg/cu (2 w/simd)", i8_fwd<I8, 84 * 1024>, true},
