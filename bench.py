@@ -393,6 +393,18 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         one[0]()
         qd = hpdct.quality_from_sums(hpdct.sums_from_buffer(sums_buf), px)
         one_ms = rms1 / steps
+        # the same with a caller-zeroed ring of per-frame sums slots
+        # (hpdct_roundtrip_u8_accumulate: no 24-byte memset kernel per launch;
+        # one memset zeroes the ring before the loop)
+        ring_n = 1024
+        ring = torch.zeros((ring_n, 3), dtype=torch.int64, device=dev)
+        acc = [hpdct.bind_roundtrip(imgs[i % args.sets], outs[i % args.sets], rt_px[i % 2], ring[i], stream=stream,
+                                    accumulate=True) for i in range(ring_n)]
+        rms2, k2, _ = timed_loop(acc, steps, 4)
+        acc_ms = rms2 / steps
+        ring.zero_()
+        acc[0]()
+        qa = hpdct.quality_from_sums(hpdct.sums_from_buffer(ring[0]), px)
         extras["c3_roundtrip"] = {
             "mse_f32": se / px, "peen_f32_pct": 100.0 * (se / sx) ** 0.5,
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
@@ -402,8 +414,11 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                              quality_from_device_sums=qd,
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums, one "
                                   "kernel; bit-identical to the two kernels"),
+            "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
+                                       note="hpdct_roundtrip_u8_accumulate into a caller-zeroed ring of 1024 "
+                                            "per-frame sums slots (one memset per ring, not per launch)"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
-        del f32_in, i8, rec, r8, x, rt_px, sums_buf
+        del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024

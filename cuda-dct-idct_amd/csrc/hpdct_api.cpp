@@ -331,8 +331,9 @@ hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_imag
     return device_status(e, "inverse kernel launch");
 }
 
-hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
-                                hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream) {
+namespace {
+hpdct_status roundtrip(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
+                       hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream, bool zero_sums) {
     static_assert(sizeof(hpdct_roundtrip_sums) == sizeof(hpdct::RtSums), "hpdct_roundtrip_sums layout");
     TileGrid g;
     if (hpdct_status st = make_grid(height, width, g)) return st;
@@ -363,9 +364,22 @@ hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_r
     const bool fast = qs.fastdiv_ok && qs.int8_ok;
     const int kind = !d_recon ? hpdct::kRtReconNone : recon_type == HPDCT_U8 ? hpdct::kRtReconU8 : hpdct::kRtReconF32;
     return device_status(hpdct::launch_roundtrip(d_image, d_coef, d_recon, kind,
-                                                 reinterpret_cast<hpdct::RtSums*>(d_sums), g, qs.qp, fast,
+                                                 reinterpret_cast<hpdct::RtSums*>(d_sums), g, qs.qp, fast, zero_sums,
                                                  static_cast<hipStream_t>(stream)),
                          "round-trip kernel launch");
+}
+}  // namespace
+
+hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
+                                hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream) {
+    return roundtrip(d_image, d_coef, d_recon, recon_type, d_sums, height, width, stream, true);
+}
+
+hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef, void* d_recon,
+                                           hpdct_dtype recon_type, hpdct_roundtrip_sums* d_sums, int64_t height,
+                                           int64_t width, void* stream) {
+    if (!d_sums) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_roundtrip_u8_accumulate needs the sums struct");
+    return roundtrip(d_image, d_coef, d_recon, recon_type, d_sums, height, width, stream, false);
 }
 
 hpdct_status hpdct_forward_u8_f32(const uint8_t* d_image, float* d_coef, int64_t height, int64_t width,

@@ -55,8 +55,9 @@ enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
 // fast: integer table in 1..255 with int8-range quotients (verified quotient,
 // packed int8 rows); sums may be nullptr (no statistics), recon nullptr with
 // kRtReconNone.  Zeroes *sums on the stream before the kernel.
+// zero_sums: hipMemsetAsync the sums before the kernel (else they accumulate)
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
-                            const TileGrid& g, const QParams& qp, bool fast, hipStream_t s);
+                            const TileGrid& g, const QParams& qp, bool fast, bool zero_sums, hipStream_t s);
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 

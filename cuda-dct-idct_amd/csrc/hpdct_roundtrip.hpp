@@ -226,8 +226,8 @@ hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, cons
 
 inline hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
                                         RtSums* sums, const TileGrid& g, const QParams& qp, bool fast,
-                                        hipStream_t s) {
-    if (sums) {
+                                        hipStream_t s, bool zero_sums = true) {
+    if (sums && zero_sums) {
         const hipError_t e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);
         if (e != hipSuccess) return e;
     }

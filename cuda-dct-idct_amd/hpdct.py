@@ -49,7 +49,7 @@ C_SYMBOLS = [
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
-    "hpdct_roundtrip_u8",
+    "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -129,8 +129,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_stream_forward.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
     lib.hpdct_baseline_forward.restype = ctypes.c_int
-    lib.hpdct_roundtrip_u8.argtypes = [vp, vp, vp, ctypes.c_int, vp, i64, i64, vp]
-    lib.hpdct_roundtrip_u8.restype = ctypes.c_int
+    for f in (lib.hpdct_roundtrip_u8, lib.hpdct_roundtrip_u8_accumulate):
+        f.argtypes = [vp, vp, vp, ctypes.c_int, vp, i64, i64, vp]
+        f.restype = ctypes.c_int
     for name, mangled in COMPAT_SYMBOLS.items():
         f = getattr(lib, mangled)
         f.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp] + ([vp] if not name.endswith("_cuda") else [])
@@ -383,11 +384,17 @@ def roundtrip(image, coef=None, recon=None, *, recon_dtype=None, sums=False, hei
     return coef, recon, (sums_from_buffer(sums_buf) if sums else None)
 
 
-def bind_roundtrip(image, coef, recon=None, sums_buf=None, *, stream=None, height=None, width=None):
+def bind_roundtrip(image, coef, recon=None, sums_buf=None, *, stream=None, height=None, width=None,
+                   accumulate=False):
     """Pre-resolved round-trip launch (like bind): a zero-argument callable.
-    sums_buf: an int64 CUDA tensor of 3 elements, or None."""
+    sums_buf: an int64 CUDA tensor of 3 elements, or None.  accumulate=True:
+    the frame's sums are added to sums_buf, which the caller zeroes
+    (hpdct_roundtrip_u8_accumulate: no per-launch memset)."""
+    if accumulate and sums_buf is None:
+        raise HpdctError(1, "accumulate=True needs a sums buffer")
     args = _roundtrip_args(image, coef, recon, sums_buf, height, width, stream)
-    fn = load_library().hpdct_roundtrip_u8
+    lib = load_library()
+    fn = lib.hpdct_roundtrip_u8_accumulate if accumulate else lib.hpdct_roundtrip_u8
 
     def call():
         st = fn(*args)

@@ -150,6 +150,16 @@ typedef struct hpdct_roundtrip_sums {
 hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
                                 hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream);
 
+/* The same round trip, but the frame's quality sums are ADDED to *d_sums,
+ * which the caller has zeroed (d_sums required).  hpdct_roundtrip_u8 zeroes the
+ * struct itself with a 24-byte hipMemsetAsync before each launch: a fill kernel
+ * of ~5 us plus its launch gap.  A pipeline that owns a ring of per-frame sums
+ * slots zeroes the ring once, with one memset for many frames, and gets the same
+ * per-frame sums (or a batch total, if frames share a slot). */
+hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef, void* d_recon,
+                                           hpdct_dtype recon_type, hpdct_roundtrip_sums* d_sums, int64_t height,
+                                           int64_t width, void* stream);
+
 /* Host-resident batch (BASELINE config C5): frame f (height x width uint8 at
  * h_frames[f]) -> coefficients at h_coef[f] (out_type HPDCT_F32 or HPDCT_I8),
  * pipelined over nstreams (1..16) HIP streams, each with one device input and

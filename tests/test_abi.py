@@ -233,6 +233,11 @@ def test_roundtrip_arguments_rejected(hp):
     assert rt(a, b, c, hp.U8, ctypes.c_void_p((1 << 31) + 8), 8, 8, None) == 1  # sums inside the recon
     assert b"overlap" in L.hpdct_last_error_string()
     assert ctypes.sizeof(ctypes.c_uint64 * 3) == 24  # hpdct_roundtrip_sums: three uint64
+    acc = L.hpdct_roundtrip_u8_accumulate
+    assert acc(a, b, c, hp.U8, None, 8, 8, None) == 1          # accumulate needs the sums struct
+    assert b"sums" in L.hpdct_last_error_string()
+    assert acc(a, b, c, hp.U8, s, 8, 12, None) == 1            # same validation as hpdct_roundtrip_u8
+    assert acc(a, b, c, hp.I8, s, 8, 8, None) == 2
 
 
 def test_host_rand_matches_glibc(hp, oracle):

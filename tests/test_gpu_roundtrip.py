@@ -103,8 +103,8 @@ def test_roundtrip_sums_only_and_no_sums(hp, oracle, dev):
 
 
 def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
-    """The sums are written (not accumulated) by each launch: the library's
-    per-stream accumulator is re-zeroed by the last workgroup, so back-to-back
+    """The sums are written (not accumulated) by each launch: the library
+    zeroes the struct on the launch stream before the kernel, so back-to-back
     launches of different grid sizes, a garbage-filled sums buffer, and
     launches on a second stream all give this frame's totals."""
     import torch
@@ -124,6 +124,35 @@ def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
     torch.cuda.synchronize()
     for buf, want in bufs:
         check_sums(hp.sums_from_buffer(buf), want)
+
+
+def test_roundtrip_accumulate_adds_into_caller_zeroed_sums(hp, oracle, dev):
+    """hpdct_roundtrip_u8_accumulate: no memset; each frame's sums are added to
+    the caller's struct.  A zeroed ring of per-frame slots gives the per-frame
+    totals; two frames sharing a slot give the sum of both (exact integer
+    fields, sse_f32 to the fixed-point unit); coefficients and reconstruction
+    are the same bits as hpdct_roundtrip_u8."""
+    import torch
+    a = oracle.rand_u8(64 * 512, 21).reshape(64, 512)
+    b = oracle.rand_u8(64 * 512, 22).reshape(64, 512)
+    xa, xb = to_dev(a, dev), to_dev(b, dev)
+    ring = torch.zeros((3, 3), dtype=torch.int64, device=dev)
+    coef = torch.empty(xa.shape, dtype=torch.float32, device=dev)
+    rec = torch.empty(xa.shape, dtype=torch.uint8, device=dev)
+    hp.bind_roundtrip(xa, coef, rec, ring[0], accumulate=True)()
+    hp.bind_roundtrip(xb, torch.empty_like(coef), None, ring[1], accumulate=True)()
+    hp.bind_roundtrip(xa, torch.empty_like(coef), None, ring[2], accumulate=True)()
+    hp.bind_roundtrip(xb, torch.empty_like(coef), None, ring[2], accumulate=True)()
+    torch.cuda.synchronize()
+    sa, sb, sab = (hp.sums_from_buffer(ring[i]) for i in range(3))
+    check_sums(sa, expected(oracle, a)[3])
+    check_sums(sb, expected(oracle, b)[3])
+    assert sab["sum_x2"] == sa["sum_x2"] + sb["sum_x2"] and sab["sse_u8"] == sa["sse_u8"] + sb["sse_u8"]
+    assert sab["sse_f32"] == sa["sse_f32"] + sb["sse_f32"]
+    c2, r2, _ = hp.roundtrip(xa, recon_dtype=torch.uint8, sums=True)
+    assert bits_equal(to_host(coef), to_host(c2)) and np.array_equal(to_host(rec), to_host(r2))
+    with pytest.raises(hp.HpdctError):
+        hp.bind_roundtrip(xa, coef, None, None, accumulate=True)
 
 
 @pytest.mark.parametrize("qtab", ["jpeg_q90", "fractional", "ones", "max255", "large"])

@@ -145,6 +145,10 @@ static void validation_paths() {
     CHECK(hpdct_roundtrip_u8((uint8_t*)a, (float*)b, (char*)b + 64, HPDCT_U8, nullptr, 8, 8, nullptr) ==
           HPDCT_ERROR_INVALID_VALUE);
     CHECK(strstr(hpdct_last_error_string(), "overlap") != nullptr);
+    CHECK(hpdct_roundtrip_u8_accumulate((uint8_t*)a, (float*)b, c, HPDCT_U8, nullptr, 8, 8, nullptr) ==
+          HPDCT_ERROR_INVALID_VALUE);
+    CHECK(hpdct_roundtrip_u8_accumulate((uint8_t*)a, (float*)b, c, HPDCT_U8, s, 12, 8, nullptr) ==
+          HPDCT_ERROR_INVALID_VALUE);
     float ones[64];
     for (float& v : ones) v = 1.0f;
     CHECK(hpdct_set_quant_table(ones) == HPDCT_SUCCESS);
