@@ -1,3 +1,10 @@
+#!/usr/bin/env python3
+"""Per-shape means of the headline kernel's counters from the tools/pmc_limits.sh
+`shape*` passes (tools/shape_probe.py pmc runs 5 shapes x 24 launches in that
+order; the first 8 launches of each are skipped), normalised to 64 Mpx where a
+counter scales with pixels; also the TCC fabric-side read / write latency
+(LEVEL / REQ).  usage: tools/pmc_shape_split.py shape_sq1 shape_sq2 shape_tcc1 ...
+(directories under gpurun_out/pmc_limits/)"""
 import csv,glob,sys
 from collections import defaultdict
 dirs=sys.argv[1:]
