@@ -69,6 +69,10 @@ def parse():
                     help="rotating buffer sets per GPU (default: inputs total >= 4x the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--sustain-s", type=float, default=4.0,
+                    help="seconds of back-to-back headline launches after the timed region (0 = off): a steady "
+                         "GPU-busy phase long enough for an external utilisation sampler, reported beside the "
+                         "headline, never as it")
     ap.add_argument("--c4-size", type=int, default=16384)
     ap.add_argument("--c5-size", type=int, default=4096)
     ap.add_argument("--c5-frames", type=int, default=512)
@@ -277,6 +281,11 @@ def main():
         "parity_spot_check": parity,
         "host_wall_s": round(wall, 4),
     }
+
+    # ------------------------------------------------------------ sustained headline
+    if args.sustain_s > 0:
+        result["sustained"] = _sustained(torch, hip, fwd_calls, args.sustain_s, px, world, barrier,
+                                         max_over_ranks)
 
     # ------------------------------------------------------------ other kernels of the path
     if not args.no_extras:
@@ -513,6 +522,33 @@ def _line(px, ms_step, kern_ms, bpp, world, pmc_key=None, n=None):
         out["traffic"] = k["hbm_bytes_per_launch"]
         out["traffic_over_algorithmic"] = k["traffic_over_algorithmic"]
     return out
+
+
+def _sustained(torch, hip, calls, seconds, px, world, barrier, max_over_ranks):
+    """The headline launches back to back for `seconds` of wall time (chunks of
+    64, one host sync per chunk so the queue stays bounded), timed by the same
+    HIP event pair.  It keeps the GPU busy long enough for a utilisation
+    sampler outside the process to see it, and shows the headline rate holds
+    over thousands of launches (clocks and power at steady state)."""
+    barrier()
+    torch.cuda.synchronize()
+    i, t0 = 0, time.perf_counter()
+    hip.record(0)
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(64):
+            calls[i % len(calls)]()
+            i += 1
+        torch.cuda.synchronize()
+    hip.record(1)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier()
+    ms = hip.elapsed(0, 1)
+    us = max_over_ranks(ms * 1e3 / i)  # the slowest rank's time per launch
+    return {"seconds": round(wall, 3), "launches_rank0": i, "us_per_launch_max_rank": round(us, 2),
+            "gpx_s": round(world * px / (us * 1e-6) / 1e9, 3),
+            "note": "headline kernel back to back for the whole period, incl. one host sync per 64 launches; "
+                    "whole job = ranks x the slowest rank's rate"}
 
 
 def _steady_ms(torch, calls, steps, stream):

@@ -117,3 +117,37 @@ def test_world_size_mismatch_is_an_error(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "1")
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
     assert bench.main() == 2
+
+
+def test_sustained_phase_reports_the_slowest_rank_rate():
+    """The sustained headline phase (a GPU-busy period long enough for an
+    outside sampler) launches in chunks until its wall time is spent and
+    rates the whole job from the slowest rank's time per launch."""
+    launched = []
+
+    class FakeTorch:
+        class cuda:
+            @staticmethod
+            def synchronize():
+                pass
+
+    class FakeHip:
+        def record(self, i):
+            pass
+
+        def elapsed(self, a, b):  # 50 us per launch on this rank
+            return len(launched) * 0.05
+
+    calls = [lambda: launched.append(1)]
+    res = bench._sustained(FakeTorch, FakeHip(), calls, 0.01, 8192 * 8192, 2, lambda: None,
+                           lambda x: 2 * x)  # the other rank is twice as slow
+    assert res["launches_rank0"] == len(launched) and len(launched) % 64 == 0 and len(launched) > 0
+    assert res["us_per_launch_max_rank"] == pytest.approx(100.0)
+    assert res["gpx_s"] == pytest.approx(2 * 8192 * 8192 / 100e-6 / 1e9, rel=1e-3)
+
+
+def test_sustained_phase_default_on_and_switchable(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    assert bench.parse().sustain_s > 0
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--sustain-s", "0"])
+    assert bench.parse().sustain_s == 0
