@@ -88,12 +88,21 @@ __device__ __forceinline__ uint32_t pack_u8x4(float a, float b, float c, float d
     return w;
 }
 
+// copysign(0.49999997f, x) as one v_bitop3_b32 (select: magnitude bits from
+// the constant, sign bit from x).  The compiler's copysign is a v_bfi_b32,
+// which issues at ~1.6x the cost of a v_bitop3_b32 / v_fma_f32 on gfx950
+// (tools/valu_rate.hip, profiles/r02/s4/valu_rate.log).
+__device__ __forceinline__ float signed_half(float x) {
+    return __uint_as_float(
+        __builtin_amdgcn_bitop3_b32(0x7fffffffu, __float_as_uint(0.49999997f), __float_as_uint(x), 0xca));
+}
+
 // roundf (round half away from zero) in three operations:
 //   trunc(x + copysign(0.49999997f, x))
 // bit-identical to roundf for all 2^32 fp32 inputs (NaN stays NaN); checked
 // exhaustively by tests/tools/verify_round3.c (tests/test_tools.py).
 __device__ __forceinline__ float round_half_away(float x) {
-    return __builtin_truncf(x + __builtin_copysignf(0.49999997f, x));
+    return __builtin_truncf(x + signed_half(x));
 }
 
 // the quotient C / Q (IEEE, or the verified 3-op form)
@@ -113,7 +122,7 @@ __device__ __forceinline__ float quotient(float c, float q, float r) {
 // and v_cvt_i32_f32 truncates, so the trunc is folded into the conversion;
 // each conversion writes its byte of the packed dword directly (SDWA dst_sel).
 __device__ __forceinline__ uint32_t pack_q_i8x4(float a, float b, float c, float d) {
-    auto biased = [](float x) { return x + __builtin_copysignf(0.49999997f, x); };
+    auto biased = [](float x) { return x + signed_half(x); };
     uint32_t w;
     asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD"
                  : "=v"(w) : "v"(biased(a)));

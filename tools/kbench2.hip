@@ -273,6 +273,15 @@ int main(int argc, char** argv) {
         {"mfma", "fwd u8->i8 MFMA first pass", mfma_i8_fwd<true>, true},
         {"mfma", "fwd u8->i8 MFMA first pass, IEEE quotient", mfma_i8_fwd<false>, true},
         {"mfma", "fwd u8->i8 library tile kernel again", prod_i8_fwd<I8>, true},
+        // copysign as v_bitop3_b32 (library) against v_bfi_b32 (the ab:: copy)
+        {"b3", "fwd u8->i8 ab copy (bfi)", i8_fwd<I8>, true},
+        {"b3", "fwd u8->i8 library (bitop3)", prod_i8_fwd<I8>, true},
+        {"b3", "fwd u8->i8 ab copy (bfi) again", i8_fwd<I8>, true},
+        {"b3", "fwd u8->i8 library (bitop3) again", prod_i8_fwd<I8>, true},
+        {"b3f", "fwd u8->f32 ab copy (bfi)", f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"b3f", "fwd u8->f32 library (bitop3)", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"b3f", "fwd u8->f32 ab copy (bfi) again", f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"b3f", "fwd u8->f32 library (bitop3) again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"i8", "fwd u8->i8 no load (diag)", i8_fwd<I8 | ab::kVarNoLoad>, false},
         {"i8", "fwd u8->i8 no store (diag)", i8_fwd<I8 | ab::kVarNoStore>, false},
         {"i8", "fwd u8->i8 math only (diag)", i8_fwd<I8 | ab::kVarNoLoad | ab::kVarNoStore>, false},
@@ -288,7 +297,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> ref(px * 4), got(px * 4);
         std::string cur;
         for (auto& v : vars) {
-            const size_t nb = v.group == "wide" || v.group == "tlb" ? px * 4 : px;  // fp32 output plane
+            const size_t nb = v.group == "wide" || v.group == "tlb" || v.group == "b3f" ? px * 4 : px;  // fp32 output plane
             CK(hipMemset(out[2], 0xa5, nb));
             v.launch(src(v, 1), out[2], c, 0);
             const hipError_t le = hipGetLastError();
@@ -375,7 +384,7 @@ int main(int argc, char** argv) {
         if (t.empty()) continue;
         std::sort(t.begin(), t.end());
         const double med = t[t.size() / 2];
-        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" ? 5.0 : 2.0;
+        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" || vars[v].group == "b3f" ? 5.0 : 2.0;
         if (vars[v].group == "rt") {
             const std::string& nm = vars[v].name;
             bpp = nm.find("(10 B") != std::string::npos  ? 10.0
