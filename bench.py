@@ -460,6 +460,27 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         line["note"] = f"{nb} 1024^2 frames per launch, stacked (C-ABI batch layout), {nbs} rotating sets"
         extras["c2_batched_fwd_u8_f32"] = line
         del c2b_in, c2b_out
+        # C2 frames as a LIST of separately allocated 1024^2 planes
+        # (hpdct_forward_frames): 64 frames per call = one launch, lists rotated
+        # over sets_for() so the inputs come from HBM
+        nf = 64
+        nls = sets_for(nf * c2 * c2)
+        fl_in = [[torch.empty((c2, c2), dtype=torch.uint8, device=dev) for _ in range(nf)] for _ in range(nls)]
+        for s, lst in enumerate(fl_in):
+            for k, t in enumerate(lst):
+                hpdct.fill_hash_u8(t, seed=7000 + 100 * s + k)
+        fl_out = [[torch.empty((c2, c2), dtype=torch.float32, device=dev) for _ in range(nf)] for _ in range(nls)]
+        calls = [hpdct.bind_frames(fl_in[s], fl_out[s], stream=stream) for s in range(nls)]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        line = _line(nf * c2 * c2, rms / steps, float(k.mean()), BYTES_PER_PX["u8_f32"], world)
+        line["us_per_frame"] = round(rms / steps / nf * 1e3, 3)
+        ok = all(torch.equal(hpdct.forward(fl_in[0][j]).view(torch.int32), fl_out[0][j].view(torch.int32))
+                 for j in (0, nf - 1))
+        line["equals_per_frame_forward"] = ok
+        line["note"] = (f"{nf} separately allocated 1024^2 frames per call (hpdct_forward_frames, one launch), "
+                        f"{nls} rotating lists")
+        extras["c2_frame_list_fwd_u8_f32"] = line
+        del fl_in, fl_out, calls
         torch.cuda.empty_cache()
         if not args.no_c4c5:
             extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks,

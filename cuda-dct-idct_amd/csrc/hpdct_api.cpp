@@ -7,11 +7,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "hpdct.h"
 #include "hpdct_kernels.h"
@@ -24,6 +26,9 @@ namespace {
 using hpdct::Mat64;
 using hpdct::QParams;
 using hpdct::TileGrid;
+using hpdct::FrameTable;
+using hpdct::kMaxFramesPerLaunch;
+using hpdct::launch_fdct_frames;
 
 // JPEG luminance table and the HpApprDCT matrix (main_newAppr.cu:60-81): the
 // same constexpr arrays the kernels compile into immediates (hpdct_tables.h).
@@ -268,6 +273,67 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     }
 #undef FWD
     return device_status(e, "forward kernel launch");
+}
+
+hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d_coefs, hpdct_dtype out_type,
+                                  int64_t n_frames, int64_t height, int64_t width, void* stream) {
+    TileGrid g;
+    if (hpdct_status st = make_grid(height, width, g)) return st;
+    if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "negative frame count");
+    if (n_frames == 0) return HPDCT_SUCCESS;
+    if (!d_images || !d_coefs) return fail(HPDCT_ERROR_INVALID_VALUE, "null frame or coefficient pointer table");
+    if (out_type != HPDCT_F32 && out_type != HPDCT_I8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "frame-list output must be HPDCT_F32 or HPDCT_I8");
+    const size_t in_bytes = static_cast<size_t>(height) * width;
+    const size_t out_bytes = in_bytes * elem_size(out_type);
+    // every plane as a byte interval; a coefficient plane may overlap nothing
+    struct Span {
+        uintptr_t a, b;
+        bool write;
+    };
+    std::vector<Span> spans;
+    spans.reserve(static_cast<size_t>(n_frames) * 2);
+    for (int64_t f = 0; f < n_frames; ++f) {
+        if (!d_images[f] || !d_coefs[f])
+            return fail(HPDCT_ERROR_INVALID_VALUE, "null device pointer for frame " + std::to_string(f));
+        if (!aligned(d_images[f], 8) || !aligned(d_coefs[f], row_align(out_type)))
+            return fail(HPDCT_ERROR_INVALID_VALUE, "frame " + std::to_string(f) +
+                                                       ": device pointers must be 8-byte (uint8 / int8) / "
+                                                       "16-byte (fp32) aligned");
+        const uintptr_t i = reinterpret_cast<uintptr_t>(d_images[f]), o = reinterpret_cast<uintptr_t>(d_coefs[f]);
+        spans.push_back({i, i + in_bytes, false});
+        spans.push_back({o, o + out_bytes, true});
+    }
+    std::sort(spans.begin(), spans.end(), [](const Span& x, const Span& y) { return x.a < y.a; });
+    for (size_t k = 0; k < spans.size(); ++k)
+        for (size_t j = k + 1; j < spans.size() && spans[j].a < spans[k].b; ++j)
+            if (spans[k].write || spans[j].write)
+                return fail(HPDCT_ERROR_INVALID_VALUE, "a coefficient plane overlaps another frame's plane");
+    const QState qs = current_qstate();
+    if (out_type == HPDCT_I8 && !qs.int8_ok)
+        return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    for (int64_t f0 = 0; f0 < n_frames; f0 += kMaxFramesPerLaunch) {
+        const int n = static_cast<int>(std::min<int64_t>(kMaxFramesPerLaunch, n_frames - f0));
+        hipError_t e;
+        if (out_type == HPDCT_F32) {
+            FrameTable<float> ft{};
+            for (int k = 0; k < n; ++k) {
+                ft.in[k] = d_images[f0 + k];
+                ft.out[k] = static_cast<float*>(d_coefs[f0 + k]);
+            }
+            e = launch_fdct_frames<float>(ft, n, g, qs.qp, qs.fastdiv_ok, s);
+        } else {
+            FrameTable<int8_t> ft{};
+            for (int k = 0; k < n; ++k) {
+                ft.in[k] = d_images[f0 + k];
+                ft.out[k] = static_cast<int8_t*>(d_coefs[f0 + k]);
+            }
+            e = launch_fdct_frames<int8_t>(ft, n, g, qs.qp, qs.fastdiv_ok, s);
+        }
+        if (e != hipSuccess) return device_status(e, "frame-list forward launch");
+    }
+    return HPDCT_SUCCESS;
 }
 
 hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_image, hpdct_dtype out_type,

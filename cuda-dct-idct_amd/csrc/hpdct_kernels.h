@@ -59,6 +59,20 @@ enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, bool fast, bool zero_sums, hipStream_t s);
 
+// A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch
+// device pointer pairs travel in the kernel arguments (1 KiB).
+constexpr int kMaxFramesPerLaunch = 64;
+template <typename TOut>
+struct FrameTable {
+    const uint8_t* in[kMaxFramesPerLaunch];
+    TOut* out[kMaxFramesPerLaunch];
+};
+// n <= kMaxFramesPerLaunch frames of grid g, uint8 -> TOut (float or int8_t),
+// built-in T, quantised with q (fastdiv as launch_fdct).
+template <typename TOut>
+hipError_t launch_fdct_frames(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, bool fastdiv,
+                              hipStream_t s);
+
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.

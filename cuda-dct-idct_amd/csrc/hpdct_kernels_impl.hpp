@@ -442,9 +442,9 @@ __device__ __forceinline__ bool wave_tame(const float (&x)[8][8]) {
 // Forward: image -> (quantised) coefficients.
 // ---------------------------------------------------------------------------
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
-__global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
-                                                            float* __restrict__ shifted, TileGrid g,
-                                                            const float* __restrict__ t_dev, QParams qp, float shift) {
+__device__ __forceinline__ void fdct_body(const TIn* __restrict__ img, TOut* __restrict__ out,
+                                          float* __restrict__ shifted, const TileGrid& g,
+                                          const float* __restrict__ t_dev, const QParams& qp, float shift) {
     // finite inputs (u8) may skip the zero terms of the built-in T
     constexpr bool kSkipZero = std::is_same_v<TIn, uint8_t>;
     const TSource<kBuiltinT, kSkipZero> T(t_dev);
@@ -477,6 +477,24 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __rest
             fdct_tile(T, x, emit);
         }
     });
+}
+
+template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
+__global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
+                                                            float* __restrict__ shifted, TileGrid g,
+                                                            const float* __restrict__ t_dev, QParams qp, float shift) {
+    fdct_body<TIn, TOut, kQuant, kBuiltinT, kWriteback, kVar>(img, out, shifted, g, t_dev, qp, shift);
+}
+
+// A list of independent, equally sized uint8 frames in one launch
+// (hpdct_forward_frames): frame blockIdx.y, its pointers from the table in
+// the kernel arguments; per frame exactly fdct_kernel's work (built-in T,
+// quantised, level shift 128), so the output is bit-identical to one launch
+// per frame.
+template <typename TOut, unsigned kVar>
+__global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_frames_kernel(FrameTable<TOut> ft, TileGrid g, QParams qp) {
+    const uint32_t f = blockIdx.y;
+    fdct_body<uint8_t, TOut, true, true, false, kVar>(ft.in[f], ft.out[f], nullptr, g, nullptr, qp, 128.0f);
 }
 
 // ---------------------------------------------------------------------------

@@ -269,6 +269,28 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
     return idct_go<kV, TIn, TOut, kDequant, kBuiltinT>(coef, out, dq_out, g, t_dev, q, shift, s);
 }
 
+// Frame lists: the tile kernel's product variant per frame (512-thread
+// workgroups), the straddle-capable stores for fp32 rows at widths that are
+// not a multiple of 512 px; grid (workgroups per frame, frames).
+template <unsigned kV, typename TOut>
+hipError_t fdct_frames_go(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, hipStream_t s) {
+    const dim3 grid(grid_for(g, false, 0, kBlock<kV>).x, static_cast<uint32_t>(n));
+    hipLaunchKernelGGL((fdct_frames_kernel<TOut, kV>), grid, dim3(kBlock<kV>), 0, s, ft, g, q);
+    return hipGetLastError();
+}
+
+template <typename TOut>
+hipError_t launch_fdct_frames_impl(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q,
+                                   bool fastdiv, hipStream_t s) {
+    constexpr unsigned kBase = kProdVar<uint8_t, TOut>;
+    if constexpr (std::is_same_v<TOut, float>) {
+        if (g.tiles_x % 64u != 0u)
+            return fastdiv ? fdct_frames_go<kBase | kVarFastDiv | kVarStraddle>(ft, n, g, q, s)
+                           : fdct_frames_go<kBase | kVarStraddle>(ft, n, g, q, s);
+    }
+    return fastdiv ? fdct_frames_go<kBase | kVarFastDiv>(ft, n, g, q, s) : fdct_frames_go<kBase>(ft, n, g, q, s);
+}
+
 inline hipError_t launch_fill_hash_impl(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {
     const uint64_t lanes = (n + 15) / 16;
     const dim3 grid(static_cast<uint32_t>((lanes + kBlockThreads - 1) / kBlockThreads));

@@ -49,7 +49,7 @@ C_SYMBOLS = [
     "hpdct_forward_u8_f32", "hpdct_forward_u8_i8", "hpdct_inverse_f32_f32",
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
-    "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate",
+    "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate", "hpdct_forward_frames",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -127,6 +127,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_get_mapping.restype = ctypes.c_int
     lib.hpdct_stream_forward.argtypes = [vp, vp, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp]
     lib.hpdct_stream_forward.restype = ctypes.c_int
+    lib.hpdct_forward_frames.argtypes = [vp, vp, ctypes.c_int, i64, i64, i64, vp]
+    lib.hpdct_forward_frames.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
     lib.hpdct_baseline_forward.restype = ctypes.c_int
     for f in (lib.hpdct_roundtrip_u8, lib.hpdct_roundtrip_u8_accumulate):
@@ -421,6 +423,65 @@ def baseline_forward(kind: str, image, tmp, result, transform, stream=None) -> N
                                                h, w, ctypes.c_void_p(transform.data_ptr()), _stream_ptr(stream))
     if st:
         raise HpdctError(st, "baseline launch failed")
+
+
+def _frame_list(frames, outs, out_dtype):
+    """Checks of one frame list (the C-ABI sees only the pointer tables):
+    every frame a contiguous uint8 CUDA tensor of one shape on one device,
+    every out a contiguous plane of h*w elements of one coefficient dtype."""
+    torch = _torch()
+    frames = list(frames)
+    if not frames:
+        return frames, [], 0, 0
+    _device_plane(frames[0], "frame 0", None, 0, (torch.uint8,))
+    h, w = _hw(frames[0], None, None)
+    shape, dev = tuple(frames[0].shape), frames[0].device
+    for i, f in enumerate(frames):
+        _device_plane(f, f"frame {i}", dev, h * w, (torch.uint8,))
+        if tuple(f.shape) != shape:
+            raise HpdctError(1, f"frame {i}: shape {tuple(f.shape)}, frame 0 is {shape}")
+    if outs is None:
+        outs = [torch.empty(shape, dtype=out_dtype or torch.float32, device=dev) for _ in frames]
+    outs = list(outs)
+    if len(outs) != len(frames):
+        raise HpdctError(1, f"{len(frames)} frames but {len(outs)} coefficient planes")
+    odt = outs[0].dtype
+    for i, o in enumerate(outs):
+        _device_plane(o, f"out {i}", dev, h * w, (torch.float32, torch.int8))
+        if o.dtype != odt:
+            raise HpdctError(1, f"out {i}: dtype {o.dtype}, out 0 is {odt}")
+    return frames, outs, h, w
+
+
+def forward_frames(frames, outs=None, *, out_dtype=None, stream=None):
+    """A list of independent uint8 frames (CUDA tensors of one shape, need not
+    be contiguous with each other) -> their quantised coefficients, one kernel
+    launch per 64 frames (hpdct_forward_frames).  Built-in T, library Q.
+    Bit-identical to forward() per frame; returns the list of outs."""
+    frames, outs, h, w = _frame_list(frames, outs, out_dtype)
+    n = len(frames)
+    if n == 0:
+        return outs
+    fp = (ctypes.c_void_p * n)(*[f.data_ptr() for f in frames])
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    _check(load_library().hpdct_forward_frames(fp, op, _dtype_code(outs[0]), n, h, w, _stream_ptr(stream)))
+    return outs
+
+
+def bind_frames(frames, outs, *, stream=None):
+    """forward_frames with every argument resolved once: a zero-argument
+    callable (bench.py's timed loop)."""
+    frames, outs, h, w = _frame_list(frames, outs, None)
+    n = len(frames)
+    fp = (ctypes.c_void_p * n)(*[f.data_ptr() for f in frames])
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    fn, args = load_library().hpdct_forward_frames, (fp, op, _dtype_code(outs[0]), n, h, w, _stream_ptr(stream))
+
+    def call():
+        st = fn(*args)
+        if st:
+            _check(st)
+    return call
 
 
 def stream_forward(frames, outs, nstreams: int = 3) -> float:

@@ -160,6 +160,21 @@ hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef
                                            hpdct_dtype recon_type, hpdct_roundtrip_sums* d_sums, int64_t height,
                                            int64_t width, void* stream);
 
+/* A list of independent device frames in as few launches as possible (config
+ * C2's small frames: one 1024^2 frame per launch is dispatch-bound, ~3.6 us for
+ * ~0.9 us of work).  d_images / d_coefs: HOST arrays of n_frames DEVICE
+ * pointers; frame f is height x width uint8 at d_images[f] (8-byte aligned),
+ * its coefficients go to d_coefs[f] as out_type HPDCT_F32 (16-byte aligned) or
+ * HPDCT_I8 (8-byte aligned).  Frames need not be contiguous or distinct inputs
+ * (a pool may repeat), but no coefficient plane may overlap another plane or
+ * any input.  Built-in T, the library Q, level shift 128: the result is
+ * bit-identical to n_frames calls of hpdct_forward.  One kernel launch per 64
+ * frames (the pointer table travels in the kernel arguments); asynchronous on
+ * `stream`; n_frames == 0 is a no-op.  The reference has no batch entry
+ * (dct_all_blocks_cuda takes one image, main_newAppr.cu:252). */
+hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d_coefs, hpdct_dtype out_type,
+                                  int64_t n_frames, int64_t height, int64_t width, void* stream);
+
 /* Host-resident batch (BASELINE config C5): frame f (height x width uint8 at
  * h_frames[f]) -> coefficients at h_coef[f] (out_type HPDCT_F32 or HPDCT_I8),
  * pipelined over nstreams (1..16) HIP streams, each with one device input and

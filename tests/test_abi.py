@@ -240,6 +240,32 @@ def test_roundtrip_arguments_rejected(hp):
     assert acc(a, b, c, hp.I8, s, 8, 8, None) == 2
 
 
+def test_forward_frames_arguments_rejected(hp):
+    """hpdct_forward_frames validates the whole pointer table before any
+    device work (no GPU here): shape, counts, nulls, alignment, overlaps."""
+    L = hp.load_library()
+    P = ctypes.c_void_p * 3
+    ins = P(1 << 20, 1 << 21, 1 << 20)           # a repeated input is allowed
+    outs = P(1 << 30, (1 << 30) + (1 << 22), 1 << 31)
+    ff = L.hpdct_forward_frames
+    assert ff(ins, outs, hp.F32, 0, 64, 64, None) == 0   # empty list: no-op
+    assert ff(ins, outs, hp.F32, -1, 64, 64, None) == 1
+    assert ff(ins, outs, hp.F32, 3, 64, 60, None) == 1   # width not a multiple of 8
+    assert ff(None, outs, hp.F32, 3, 64, 64, None) == 1
+    assert ff(ins, outs, hp.U8, 3, 64, 64, None) == 2    # coefficients are f32 or i8
+    assert ff(P(1 << 20, None, 1 << 20), outs, hp.F32, 3, 64, 64, None) == 1
+    assert ff(P(1 << 20, (1 << 21) + 4, 1 << 20), outs, hp.F32, 3, 64, 64, None) == 1  # misaligned frame
+    assert ff(ins, P(1 << 30, (1 << 30) + (1 << 22) + 8, 1 << 31), hp.F32, 3, 64, 64, None) == 1  # f32: 16 B
+    assert ff(ins, P(1 << 30, (1 << 30) + 64, 1 << 31), hp.F32, 3, 64, 64, None) == 1  # two outs overlap
+    assert b"overlap" in L.hpdct_last_error_string()
+    assert ff(ins, P(1 << 30, (1 << 21) + 64, 1 << 31), hp.I8, 3, 64, 64, None) == 1  # out inside an input
+    hp.set_quant_table(np.ones(64, np.float32))
+    try:
+        assert ff(ins, outs, hp.I8, 3, 64, 64, None) == 3  # int8 overflow with this table
+    finally:
+        hp.set_quant_table(None)
+
+
 def test_host_rand_matches_glibc(hp, oracle):
     assert np.array_equal(hp.fill_rand_u8(100000, 42), oracle.rand_u8(100000, 42))
     assert np.array_equal(hp.fill_rand_u8(5000, 7), oracle.rand_u8(5000, 7))

@@ -1,0 +1,90 @@
+"""GPU parity of hpdct_forward_frames: a list of separately allocated uint8
+frames in one launch per 64 frames (the answer to config C2's dispatch-bound
+single-frame launches; the reference has no batch entry, dct_all_blocks_cuda
+takes one image, main_newAppr.cu:252).
+
+Every frame's coefficients must equal hpdct_forward on that frame alone BIT FOR
+BIT, and sampled frames equal the CPU oracle (the checker only).  Cases: more
+than 64 frames (two launches, the second ragged), a width that is not a
+multiple of 512 px (the straddle-capable stores), the C2 1024^2 frame size in
+fp32 and int8, an input pool repeated across the list, and a custom integer
+quant table (the verified fast quotient) against an IEEE-division one.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(hp, dev, n, h, w, seed0):
+    import torch
+    out = []
+    for k in range(n):
+        x = torch.empty((h, w), dtype=torch.uint8, device=dev)
+        hp.fill_hash_u8(x, seed=seed0 + k)
+        out.append(x)
+        # a spacer allocation so the frames are not one contiguous plane
+        out.append(torch.empty(4096 + 64 * k, dtype=torch.uint8, device=dev))
+    return out[0::2]
+
+
+def _bits(t):
+    import torch
+    return t.view(torch.int32) if t.dtype == torch.float32 else t
+
+
+@pytest.mark.parametrize("out_dtype", ["float32", "int8"])
+@pytest.mark.parametrize("h,w,n", [(64, 136, 70), (1024, 1024, 33), (48, 4096, 3), (8, 8, 1)])
+def test_frames_equal_per_frame_forward(hp, dev, out_dtype, h, w, n):
+    import torch
+    dt = getattr(torch, out_dtype)
+    frames = _frames(hp, dev, n, h, w, seed0=100 + h + w)
+    outs = hp.forward_frames(frames, out_dtype=dt)
+    for k, (x, y) in enumerate(zip(frames, outs)):
+        ref = hp.forward(x, out_dtype=dt)
+        assert torch.equal(_bits(ref), _bits(y)), f"frame {k} of {n} ({h}x{w}, {out_dtype})"
+
+
+def test_frames_vs_oracle_and_repeated_pool(hp, oracle, dev):
+    import torch
+    pool = _frames(hp, dev, 3, 64, 1040, seed0=7)
+    frames = [pool[k % 3] for k in range(130)]  # inputs repeat; outputs are distinct
+    outs = hp.forward_frames(frames)
+    torch.cuda.synchronize()
+    for k in (0, 1, 2, 64, 65, 129):
+        ref = oracle.fdct(frames[k].cpu().numpy())
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}"
+    for k in range(3, 130):
+        assert torch.equal(_bits(outs[k]), _bits(outs[k % 3]))
+
+
+@pytest.mark.parametrize("table", ["integer", "fractional"])
+def test_frames_custom_quant_table(hp, oracle, dev, table):
+    """Integer table in 1..255: the verified 3-op quotient; fractional: IEEE
+    division.  Both must match the oracle under that table."""
+    import torch
+    q = np.arange(1, 65, dtype=np.float32) * (1.0 if table == "integer" else 1.37)
+    hp.set_quant_table(q)
+    try:
+        frames = _frames(hp, dev, 5, 16, 512, seed0=900)
+        outs = hp.forward_frames(frames)
+        torch.cuda.synchronize()
+        for k, (x, y) in enumerate(zip(frames, outs)):
+            ref = oracle.fdct(x.cpu().numpy(), Q=q)
+            assert np.array_equal(y.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"frame {k}"
+    finally:
+        hp.set_quant_table(None)
+
+
+def test_frames_on_a_side_stream(hp, dev):
+    import torch
+    s = torch.cuda.Stream()
+    frames = _frames(hp, dev, 4, 256, 256, seed0=55)
+    torch.cuda.synchronize()
+    outs = [torch.empty((256, 256), dtype=torch.float32, device=dev) for _ in frames]
+    with torch.cuda.stream(s):
+        call = hp.bind_frames(frames, outs, stream=s)
+        call()
+    s.synchronize()
+    for x, y in zip(frames, outs):
+        assert torch.equal(_bits(hp.forward(x)), _bits(y))

@@ -149,3 +149,23 @@ def test_fill_hash_checks_its_plane(hp, t):
         hp.fill_hash_u8(FakeDev((64,), t.float32), seed=1)
     with pytest.raises(hp.HpdctError):
         hp.fill_hash_u8(t.zeros(64, dtype=t.uint8), seed=1)  # host tensor
+
+
+def test_forward_frames_checks_every_plane(hp, t):
+    f = FakeDev((64, 64), t.uint8)
+    o = FakeDev((64, 64), t.float32)
+    with pytest.raises(hp.HpdctError, match="shape"):
+        hp.forward_frames([f, FakeDev((32, 128), t.uint8)], [o, o])
+    with pytest.raises(hp.HpdctError):
+        hp.forward_frames([f, FakeDev((64, 64), t.float32)], [o, o])
+    with pytest.raises(hp.HpdctError, match="coefficient planes"):
+        hp.forward_frames([f, f], [o])
+    with pytest.raises(hp.HpdctError, match="holds"):
+        hp.forward_frames([f], [FakeDev((64, 32), t.float32)])
+    with pytest.raises(hp.HpdctError, match="dtype"):
+        hp.forward_frames([f, f], [o, FakeDev((64, 64), t.int8)])
+    with pytest.raises(hp.HpdctError):
+        hp.forward_frames([f, FakeDev((64, 64), t.uint8, device="cuda:1")], [o, o])
+    with pytest.raises(hp.HpdctError):
+        hp.forward_frames([FakeDev((64, 64), t.uint8, contiguous=False)], [o])
+    assert hp.forward_frames([], []) == []
