@@ -158,6 +158,27 @@ static void validation_paths() {
     CHECK(hpdct_fill_hash_u8((uint8_t*)a, -1, 42, 0, nullptr) == HPDCT_ERROR_INVALID_VALUE);
     CHECK(hpdct_set_mapping((hpdct_mapping)7) == HPDCT_ERROR_INVALID_VALUE);
 
+    // hpdct_forward_frames: the pointer-table checks (exact-size host tables;
+    // the device pointers are never dereferenced on the host)
+    {
+        const uint8_t** fin = exact<const uint8_t*>(3);
+        void** fout = exact<void*>(3);
+        fin[0] = (const uint8_t*)(uintptr_t(1) << 20), fin[1] = (const uint8_t*)(uintptr_t(1) << 21), fin[2] = fin[0];
+        fout[0] = (void*)(uintptr_t(1) << 30), fout[1] = (void*)((uintptr_t(1) << 30) + (1u << 22));
+        fout[2] = (void*)(uintptr_t(1) << 31);
+        CHECK(hpdct_forward_frames(fin, fout, HPDCT_F32, 0, 64, 64, nullptr) == HPDCT_SUCCESS);
+        CHECK(hpdct_forward_frames(fin, fout, HPDCT_F32, -3, 64, 64, nullptr) == HPDCT_ERROR_INVALID_VALUE);
+        CHECK(hpdct_forward_frames(nullptr, fout, HPDCT_F32, 3, 64, 64, nullptr) == HPDCT_ERROR_INVALID_VALUE);
+        CHECK(hpdct_forward_frames(fin, fout, HPDCT_U8, 3, 64, 64, nullptr) == HPDCT_ERROR_UNSUPPORTED);
+        fout[1] = (void*)((uintptr_t(1) << 30) + 64);  // overlaps out 0
+        CHECK(hpdct_forward_frames(fin, fout, HPDCT_F32, 3, 64, 64, nullptr) == HPDCT_ERROR_INVALID_VALUE);
+        CHECK(strstr(hpdct_last_error_string(), "overlap") != nullptr);
+        fout[1] = nullptr;
+        CHECK(hpdct_forward_frames(fin, fout, HPDCT_I8, 3, 64, 64, nullptr) == HPDCT_ERROR_INVALID_VALUE);
+        free(fin);
+        free(fout);
+    }
+
     // hpdct_stream_forward: every check that precedes stream creation
     std::vector<uint8_t> px(64 * 64);
     std::vector<float> out(64 * 64);
