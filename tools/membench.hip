@@ -90,6 +90,68 @@ __global__ __launch_bounds__(256) void mix_run(const uint32_t* __restrict__ in, 
     for (uint32_t k = 0; k < kRun / 256; ++k) st4<true>(&out[i0 + 64u * k + lane], cvt4(w[k]));
 }
 
+// The headline kernel's access pattern without its arithmetic (n x n u8 ->
+// fp32, n a multiple of 4096): wave w of the grid owns 64-tile set w (8 rows x
+// 512 px): 8 row loads of 512 B (8 B per lane), 16 NT stores of 1 KiB (two
+// per 2 KiB output row).  8 waves per workgroup.
+// kOrder 0: consecutive waves along the tile row; 1: consecutive waves down
+// the tile rows (column strips of 512 px).  kWg threads per workgroup.
+template <int kOrder, uint32_t kWg>
+__global__ __launch_bounds__(kWg) void pat_rows8(const uint8_t* __restrict__ in, float* __restrict__ out, uint32_t n) {
+    const uint32_t wave = blockIdx.x * (kWg / 64u) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t spr = n / 512u, trows = n / 8u;
+    const uint32_t ty = kOrder == 0 ? wave / spr : wave % trows, sx = kOrder == 0 ? wave - ty * spr : wave / trows;
+    const uint64_t base = (uint64_t)ty * 8u * n + (uint64_t)sx * 512u;
+    uint2 r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint2*>(in + base + (uint64_t)i * n + 8u * lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float4* row = reinterpret_cast<float4*>(out + base + (uint64_t)i * n);
+        st4<true>(row + lane, cvt4(r[i].x));
+        st4<true>(row + 64u + lane, cvt4(r[i].y));
+    }
+}
+
+// The int8 forward's access pattern without its arithmetic: 8 row loads and 8
+// NT row stores of 512 B (8 B per lane) per 64-tile set.
+__global__ __launch_bounds__(512) void pat_rows8_i8(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                    uint32_t n) {
+    const uint32_t wave = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t spr = n / 512u, ty = wave / spr, sx = wave - ty * spr;
+    const uint64_t base = (uint64_t)ty * 8u * n + (uint64_t)sx * 512u;
+    uint2 r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint2*>(in + base + (uint64_t)i * n + 8u * lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint2* p = reinterpret_cast<uint2*>(out + base + (uint64_t)i * n + 8u * lane);
+        __builtin_nontemporal_store(r[i].x ^ 0x80808080u, &p->x);
+        __builtin_nontemporal_store(r[i].y ^ 0x80808080u, &p->y);
+    }
+}
+
+// The same workgroup footprint (8 rows x 4096 px) with the work split by row:
+// wave w of the workgroup loads row w (4 KiB, 1 KiB per instruction) and
+// stores it (16 KiB, 1 KiB per instruction).
+__global__ __launch_bounds__(512) void pat_rowwave(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                   uint32_t n) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t bpr = n / 4096u, ty = blockIdx.x / bpr, bx = blockIdx.x - ty * bpr;
+    const uint64_t base = ((uint64_t)ty * 8u + w) * n + (uint64_t)bx * 4096u;
+    uint4 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const uint4*>(in + base + 1024u * k + 16u * lane);
+    float4* row = reinterpret_cast<float4*>(out + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        st4<true>(row + 256u * k + lane, cvt4(r[k].x));
+        st4<true>(row + 256u * k + 64u + lane, cvt4(r[k].y));
+        st4<true>(row + 256u * k + 128u + lane, cvt4(r[k].z));
+        st4<true>(row + 256u * k + 192u + lane, cvt4(r[k].w));
+    }
+}
+
 // write-only, each wave one contiguous run of kRun floats
 template <uint32_t kRun>
 __global__ __launch_bounds__(256) void write_run(float4* __restrict__ out, uint64_t n4) {
@@ -347,6 +409,36 @@ int main(int argc, char** argv) {
     cases.push_back({"hipMemcpyD2D 4B/px (r+w)", 8.0 * px, [=](int s) {
                          CK(hipMemcpyAsync(out[s], out[(s + 1) % nsets], px * 4, hipMemcpyDeviceToDevice, 0));
                      }});
+    if (n % 4096 == 0) {
+        cases.push_back({"pat rows8 (headline pattern)", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_rows8<0, 512>), dim3((unsigned)(px / 4096 / 8)), dim3(512), 0, 0,
+                                                (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rows8 i8 (int8 pattern)", 2.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(pat_rows8_i8, dim3((unsigned)(px / 4096 / 8)), dim3(512), 0, 0,
+                                                (const uint8_t*)in[s], (uint8_t*)out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rows8 wg1024", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_rows8<0, 1024>), dim3((unsigned)(px / 4096 / 16)), dim3(1024), 0,
+                                                0, (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rows8 wg256", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_rows8<0, 256>), dim3((unsigned)(px / 4096 / 4)), dim3(256), 0,
+                                                0, (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rows8 column strips", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_rows8<1, 512>), dim3((unsigned)(px / 4096 / 8)), dim3(512), 0, 0,
+                                                (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rowwave (row per wave)", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(pat_rowwave, dim3((unsigned)(px / 4096 / 8)), dim3(512), 0, 0,
+                                                (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"mix_run 4096 px/wave nt (pat)", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(mix_run<4096>, dim3((unsigned)(px / 4096 / 4)), dim3(256), 0, 0,
+                                                (const uint32_t*)in[s], (float4*)out[s], n4);
+                         }});
+    }
     cases.push_back({"hipMemsetD32 4B/px", 4.0 * px, [=](int s) { CK(hipMemsetD32Async((hipDeviceptr_t)out[s], 7, px, 0)); }});
 
     if (argc > 3 && strcmp(argv[3], "mix") == 0) {
@@ -354,6 +446,14 @@ int main(int argc, char** argv) {
         for (auto& c : cases)
             if (c.name.find("mix") != std::string::npos || c.name.find("write") != std::string::npos ||
                 c.name.find("Memset") != std::string::npos)
+                keep.push_back(c);
+        cases.swap(keep);
+    }
+    if (argc > 3 && strcmp(argv[3], "pat") == 0) {
+        std::vector<Case> keep;
+        for (auto& c : cases)
+            if (c.name.find("pat") != std::string::npos || c.name.find("mix_w4 nt    g8") != std::string::npos ||
+                c.name.find("copy_u8 x8 nt    g8") != std::string::npos)
                 keep.push_back(c);
         cases.swap(keep);
     }
