@@ -32,6 +32,7 @@
 #include "kbench_variants.hpp"
 #include "kbench_mfma.hpp"
 #include "hpdct_roundtrip.hpp"
+#include "kbench_linread.hpp"
 
 using namespace hpdct;
 
@@ -127,6 +128,14 @@ void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+void lin_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (!lin::linread_ok(c.g)) {
+        fprintf(stderr, "linread: width must be a multiple of 8192 px\n");
+        exit(2);
+    }
+    lin::linread_go<kVarFastDiv>(static_cast<const uint8_t*>(in), static_cast<float*>(out), c.g, c.qp, s);
 }
 
 template <bool kFast>
@@ -273,6 +282,12 @@ int main(int argc, char** argv) {
         {"mfma", "fwd u8->i8 MFMA first pass", mfma_i8_fwd<true>, true},
         {"mfma", "fwd u8->i8 MFMA first pass, IEEE quotient", mfma_i8_fwd<false>, true},
         {"mfma", "fwd u8->i8 library tile kernel again", prod_i8_fwd<I8>, true},
+        // linear 4 KiB input reads staged through LDS (kbench_linread.hpp) against the library kernel
+        {"lin", "fwd u8->f32 library (b512)", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"lin", "fwd u8->f32 linear reads via LDS (b1024)", lin_f32_fwd, true},
+        {"lin", "fwd u8->f32 library b1024", prod_f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | W1024 | F>, true},
+        {"lin", "fwd u8->f32 library (b512) again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"lin", "fwd u8->f32 linear reads via LDS again", lin_f32_fwd, true},
         // copysign as v_bitop3_b32 (library) against v_bfi_b32 (the ab:: copy)
         {"b3", "fwd u8->i8 ab copy (bfi)", i8_fwd<I8>, true},
         {"b3", "fwd u8->i8 library (bitop3)", prod_i8_fwd<I8>, true},
@@ -297,7 +312,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> ref(px * 4), got(px * 4);
         std::string cur;
         for (auto& v : vars) {
-            const size_t nb = v.group == "wide" || v.group == "tlb" || v.group == "b3f" ? px * 4 : px;  // fp32 output plane
+            const size_t nb = v.group == "wide" || v.group == "tlb" || v.group == "b3f" || v.group == "lin" ? px * 4 : px;  // fp32 output plane
             CK(hipMemset(out[2], 0xa5, nb));
             v.launch(src(v, 1), out[2], c, 0);
             const hipError_t le = hipGetLastError();
@@ -384,7 +399,7 @@ int main(int argc, char** argv) {
         if (t.empty()) continue;
         std::sort(t.begin(), t.end());
         const double med = t[t.size() / 2];
-        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" || vars[v].group == "b3f" ? 5.0 : 2.0;
+        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" || vars[v].group == "b3f" || vars[v].group == "lin" ? 5.0 : 2.0;
         if (vars[v].group == "rt") {
             const std::string& nm = vars[v].name;
             bpp = nm.find("(10 B") != std::string::npos  ? 10.0

@@ -131,6 +131,57 @@ __global__ __launch_bounds__(512) void pat_rows8_i8(const uint8_t* __restrict__ 
     }
 }
 
+// Half-and-half patterns (the values are not a transform; bandwidth only):
+// kLinRead: each wave loads 4 KiB contiguous (wave w -> bytes [4096w, +4096),
+// 4 x 1 KiB) instead of the set's 8 row pieces; kLinWrite: each wave stores
+// 16 KiB contiguous (floats [4096w, +4096)) instead of the set's 8 x 2 KiB.
+template <bool kLinRead, bool kLinWrite>
+__global__ __launch_bounds__(512) void pat_half(const uint8_t* __restrict__ in, float* __restrict__ out, uint32_t n) {
+    const uint32_t wave = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t spr = n / 512u, ty = wave / spr, sx = wave - ty * spr;
+    const uint64_t base = (uint64_t)ty * 8u * n + (uint64_t)sx * 512u;
+    const uint64_t lin = (uint64_t)wave * 4096u;
+    uint2 r[8];
+    if constexpr (kLinRead) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = *reinterpret_cast<const uint4*>(in + lin + 1024u * k + 16u * lane);
+            r[2 * k] = make_uint2(v.x, v.y);
+            r[2 * k + 1] = make_uint2(v.z, v.w);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint2*>(in + base + (uint64_t)i * n + 8u * lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float4* row = kLinWrite ? reinterpret_cast<float4*>(out + lin + 512u * i)
+                                : reinterpret_cast<float4*>(out + base + (uint64_t)i * n);
+        st4<true>(row + lane, cvt4(r[i].x));
+        st4<true>(row + 64u + lane, cvt4(r[i].y));
+    }
+}
+
+// Two sets per wave: 8 row loads of 1 KiB (16 B per lane), 8 x 4 KiB of
+// output (4 NT stores of 1 KiB per row).  8 waves per workgroup.
+__global__ __launch_bounds__(512) void pat_rows8x2(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                   uint32_t n) {
+    const uint32_t wave = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t spr = n / 1024u, ty = wave / spr, sx = wave - ty * spr;
+    const uint64_t base = (uint64_t)ty * 8u * n + (uint64_t)sx * 1024u;
+    uint4 r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const uint4*>(in + base + (uint64_t)i * n + 16u * lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float4* row = reinterpret_cast<float4*>(out + base + (uint64_t)i * n);
+        st4<true>(row + lane, cvt4(r[i].x));
+        st4<true>(row + 64u + lane, cvt4(r[i].y));
+        st4<true>(row + 128u + lane, cvt4(r[i].z));
+        st4<true>(row + 192u + lane, cvt4(r[i].w));
+    }
+}
+
 // The same workgroup footprint (8 rows x 4096 px) with the work split by row:
 // wave w of the workgroup loads row w (4 KiB, 1 KiB per instruction) and
 // stores it (16 KiB, 1 KiB per instruction).
@@ -417,6 +468,22 @@ int main(int argc, char** argv) {
         cases.push_back({"pat rows8 i8 (int8 pattern)", 2.0 * px, [=](int s) {
                              hipLaunchKernelGGL(pat_rows8_i8, dim3((unsigned)(px / 4096 / 8)), dim3(512), 0, 0,
                                                 (const uint8_t*)in[s], (uint8_t*)out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat linear reads + tile writes", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_half<true, false>), dim3((unsigned)(px / 4096 / 8)), dim3(512), 0,
+                                                0, (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat tile reads + linear writes", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_half<false, true>), dim3((unsigned)(px / 4096 / 8)), dim3(512), 0,
+                                                0, (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat linear reads + linear writes", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL((pat_half<true, true>), dim3((unsigned)(px / 4096 / 8)), dim3(512), 0,
+                                                0, (const uint8_t*)in[s], out[s], (uint32_t)n);
+                         }});
+        cases.push_back({"pat rows8 x2 (two sets per wave)", 5.0 * px, [=](int s) {
+                             hipLaunchKernelGGL(pat_rows8x2, dim3((unsigned)(px / 8192 / 8)), dim3(512), 0, 0,
+                                                (const uint8_t*)in[s], out[s], (uint32_t)n);
                          }});
         cases.push_back({"pat rows8 wg1024", 5.0 * px, [=](int s) {
                              hipLaunchKernelGGL((pat_rows8<0, 1024>), dim3((unsigned)(px / 4096 / 16)), dim3(1024), 0,
