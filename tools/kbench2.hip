@@ -91,6 +91,24 @@ void i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        128.0f);
 }
 
+// int8: two sets per wave (16 row loads up front) and persistent waves with a
+// prefetch of the next set, for the VALU/memory overlap the phase split shows
+template <unsigned kVar>
+void i8_fwd_two(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t sets = (c.g.ntiles + 63u) / 64u, per = kBlock<kVar> / 64u;
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, int8_t, true, true, false, kVar | ab::kVarTwoSets>),
+                       dim3(((sets + 1) / 2 + per - 1) / per), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp,
+                       128.0f);
+}
+template <unsigned kVar>
+void i8_fwd_persist(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((ab::fdct_kernel<uint8_t, int8_t, true, true, false, kVar | ab::kVarPersist2>),
+                       grid_for(c.g, true, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp,
+                       128.0f);
+}
+
 // ---- forward u8 -> fp32 (the headline kernel), set order A/B on wide frames
 template <unsigned kVar, uint32_t kLdsBytes = 0>
 void f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
@@ -252,6 +270,11 @@ int main(int argc, char** argv) {
         {"i8", "fwd u8->i8 lds 2 wg/cu (4 w/simd)", i8_fwd<I8, 64 * 1024>, true},
         {"i8", "fwd u8->i8 b256 lds 3 wg/cu (3 w/simd)", i8_fwd<F | N | IP, 48 * 1024>, true},
         {"i8", "fwd u8->i8 b256 lds 4 wg/cu (4 w/simd)", i8_fwd<F | N | IP, 40 * 1024>, true},
+        {"i8", "fwd u8->i8 two sets per wave", i8_fwd_two<I8>, true},
+        {"i8", "fwd u8->i8 two sets per wave b256", i8_fwd_two<F | N | IP>, true},
+        {"i8", "fwd u8->i8 persistent+prefetch", i8_fwd_persist<I8>, true},
+        {"i8", "fwd u8->i8 persistent+prefetch b256", i8_fwd_persist<F | N | IP>, true},
+        {"i8", "fwd u8->i8 (product) again", i8_fwd<I8>, true},
         {"rt", "rt two kernels fwd+inv->u8 (10 B/px)", rt_two_kernels, true},
         {"rt", "rt fused u8 recon + sums (6 B/px)", rt_fused<kRtReconU8, true, true>, true},
         {"rt", "rt fused u8 recon (6 B/px)", rt_fused<kRtReconU8, false, true>, true},
