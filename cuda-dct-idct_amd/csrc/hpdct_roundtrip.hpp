@@ -60,7 +60,9 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // profiles/r01/mappings/kbench2_rt.log)
 template <int kRecon>
 constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
-template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false>
+// kWaveAtomics: each wave adds its partials with its own 64-bit atomics (no
+// workgroup barrier in the epilogue); false: one atomic per field per workgroup
+template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false, bool kWaveAtomics = false>
 __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
@@ -180,6 +182,15 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
         unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
         unsigned long long xx = static_cast<unsigned long long>(acc_xx);
         f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
+        if constexpr (kWaveAtomics) {
+            if (lane == 0u) {
+                auto* out = reinterpret_cast<unsigned long long*>(sums);
+                if (f) atomicAdd(out + 0, f);
+                if (e8) atomicAdd(out + 1, e8);
+                if (xx) atomicAdd(out + 2, xx);
+            }
+            return;
+        }
         __shared__ unsigned long long part[512 / 64][3];
         const uint32_t w = threadIdx.x / 64u;
         if ((threadIdx.x & 63u) == 0u) part[w][0] = f, part[w][1] = e8, part[w][2] = xx;

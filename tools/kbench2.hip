@@ -186,10 +186,10 @@ void rt_fused(const void* in, void* out, const Ctx& c, hipStream_t s) {
                      kRecon, kStats ? g_sums : nullptr, c.g, c.qp, kFast, s, true);
 }
 
-template <int kRaw>
+template <int kRaw, bool kWave = false, bool kMemset = true>
 void rt_raw(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw>), roundtrip_grid(c.g), dim3(512), 0, s,
+    if (kMemset) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw, false, kWave>), roundtrip_grid(c.g), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef2[set_of(in)], out, g_sums, c.g, c.qp);
 }
 
@@ -281,6 +281,10 @@ int main(int argc, char** argv) {
         {"rt", "rt fused u8 recon + sums, raw in VGPRs", rt_raw<0>, true},
         {"rt", "rt fused u8 recon + sums, raw re-read", rt_raw<1>, true},
         {"rt", "rt fused u8 recon + sums, raw in LDS", rt_raw<2>, true},
+        {"rt", "rt fused u8 recon + sums, per-wave atomics", rt_raw<2, true>, true},
+        {"rt", "rt sums, no memset (accumulate)", rt_raw<2, false, false>, true},
+        {"rt", "rt sums, no memset, per-wave atomics", rt_raw<2, true, false>, true},
+        {"rt", "rt fused u8 recon + sums, raw in LDS again", rt_raw<2>, true},
         {"rt", "rt fused sums only (5 B/px)", rt_fused<kRtReconNone, true, true>, false},
         {"rt", "rt fused f32 recon + sums (9 B/px)", rt_fused<kRtReconF32, true, true>, false},
         {"rt", "rt fused u8 recon + sums, IEEE/fp32 q", rt_fused<kRtReconU8, true, false>, true},
