@@ -62,7 +62,10 @@ template <int kRecon>
 constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
 // kWaveAtomics: each wave adds its partials with its own 64-bit atomics (no
 // workgroup barrier in the epilogue); false: one atomic per field per workgroup
-template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false, bool kWaveAtomics = false>
+// kSpreadSums (diagnostic): workgroup b adds into sums[b] instead of sums[0]
+// (the caller passes one RtSums per workgroup), to price the same-line atomics
+template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false, bool kWaveAtomics = false,
+          bool kSpreadSums = false>
 __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
@@ -198,7 +201,8 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
         if (threadIdx.x < 3u) {
             unsigned long long s = 0;
             for (uint32_t k = 0; k < 512u / 64u; ++k) s += part[k][threadIdx.x];
-            if (s) atomicAdd(reinterpret_cast<unsigned long long*>(sums) + threadIdx.x, s);
+            RtSums* const dst = kSpreadSums ? sums + blockIdx.x : sums;
+            if (s) atomicAdd(reinterpret_cast<unsigned long long*>(dst) + threadIdx.x, s);
         }
     }
 }

@@ -186,6 +186,13 @@ void rt_fused(const void* in, void* out, const Ctx& c, hipStream_t s) {
                      kRecon, kStats ? g_sums : nullptr, c.g, c.qp, kFast, s, true);
 }
 
+// one RtSums per workgroup (diagnostic: no two workgroups add into one line)
+void rt_spread(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    static RtSums* spread = nullptr;
+    if (!spread) (void)hipMalloc(&spread, sizeof(RtSums) * roundtrip_grid(c.g).x);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, 2, false, false, true>), roundtrip_grid(c.g),
+                       dim3(512), 0, s, static_cast<const uint8_t*>(in), g_coef2[set_of(in)], out, spread, c.g, c.qp);
+}
 template <int kRaw, bool kWave = false, bool kMemset = true>
 void rt_raw(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kMemset) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
@@ -281,9 +288,11 @@ int main(int argc, char** argv) {
         {"rt", "rt fused u8 recon + sums, raw in VGPRs", rt_raw<0>, true},
         {"rt", "rt fused u8 recon + sums, raw re-read", rt_raw<1>, true},
         {"rt", "rt fused u8 recon + sums, raw in LDS", rt_raw<2>, true},
-        {"rt", "rt fused u8 recon + sums, per-wave atomics", rt_raw<2, true>, true},
         {"rt", "rt sums, no memset (accumulate)", rt_raw<2, false, false>, true},
-        {"rt", "rt sums, no memset, per-wave atomics", rt_raw<2, true, false>, true},
+        {"rt", "rt sums, no memset, one RtSums per workgroup", rt_spread, true},
+        {"rt", "rt sums, no memset (accumulate) again", rt_raw<2, false, false>, true},
+        {"rt", "rt sums, no memset, one RtSums per workgroup again", rt_spread, true},
+        {"rt", "rt fused u8 recon + sums, per-wave atomics", rt_raw<2, true>, true},
         {"rt", "rt fused u8 recon + sums, raw in LDS again", rt_raw<2>, true},
         {"rt", "rt fused sums only (5 B/px)", rt_fused<kRtReconNone, true, true>, false},
         {"rt", "rt fused f32 recon + sums (9 B/px)", rt_fused<kRtReconF32, true, true>, false},
