@@ -140,7 +140,10 @@ def main():
     local_dev = local % ndev if ndev else local
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    # a launcher (torchrun, or launch_ranks) sets WORLD_SIZE: then the process
+    # group is initialised even at WORLD_SIZE=1, so the RCCL init path runs
+    use_pg = world > 1 or "WORLD_SIZE" in os.environ
+    if use_pg:
         # collectives raise (instead of aborting the process) if a peer dies, so
         # rank 0 can still print the headline line; generous timeout
         os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
@@ -151,11 +154,11 @@ def main():
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=240))
 
     def barrier():
-        if world > 1:
+        if use_pg:
             dist.barrier()
 
     def max_over_ranks(x: float) -> float:
-        if world == 1:
+        if not use_pg:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -310,7 +313,7 @@ def main():
 
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_pg:
         try:
             dist.destroy_process_group()
         except Exception:
@@ -593,11 +596,16 @@ def _steady_ms(torch, calls, steps, stream):
 
 def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop):
     """C4: one 16384^2 frame row-sharded over the ranks (device-generated by
-    the stateless hash so no H2D), forward kernel per slab, then the RCCL
-    gather of the fp32 coefficient slabs to rank 0, timed separately."""
-    from hpdct_dist import gather_slabs, shard_rows
+    the stateless hash so no H2D), forward kernel per slab, then the gather
+    of the coefficient slabs to rank 0, timed separately.  With the nccl
+    backend the gather is the native C-ABI (include/hpdct_dist.h:
+    hpdct_gather_rows, ncclSend/ncclRecv over xGMI) on a communicator of its
+    own, at every world size including 1 (then a device-to-device copy of the
+    root's own slab); the gloo rehearsal (several ranks on one GPU, which RCCL
+    cannot serve) keeps torch.distributed's gather."""
+    from hpdct_dist import gather_slabs
     n = args.c4_size
-    r0, rows = shard_rows(n, world, rank)
+    r0, rows = hpdct.shard_rows_native(n, world, rank)
     # identical slab buffer sets, rotated: their inputs total >= 4x the
     # Infinity Cache (at 8 ranks a slab reads 32 MiB: 32 sets)
     nsl = sets_for(rows * n)
@@ -613,54 +621,69 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     out = {"frame": [n, n], "rows_per_rank": rows, "slab_sets": nsl, "compute_ms_max_rank": round(compute_ms, 4),
            "compute_gpx_s": round(n * n / (compute_ms * 1e-3) / 1e9, 2),
            "compute_hbm_frac_max_rank": round(5 * rows * n / (compute_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    if world > 1:
-        hpdct.forward(x, y)  # y = this rank's slab of the frame (set 0)
-        gather_ms = []
-        full = None
+    comm = None
+    if args.backend == "nccl":
+        if world == 1:
+            comm = hpdct.Comm.init_all([dev.index])[0]
+        else:
+            uid = [hpdct.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = hpdct.Comm.init_rank(world, uid[0], rank, dev.index)
+        out["gather_path"] = "native RCCL: hpdct_gather_rows (ncclSend/ncclRecv group), libhpdct_dist.so"
+        hpdct.forward_slab(comm, x, y, n, n, stream=stream)  # y = this rank's slab (set 0), via the C-ABI
+    else:
+        out["gather_path"] = "torch.distributed gather (gloo rehearsal, staged through host memory)"
+        hpdct.forward(x, y)
+
+    def gather(slab):
+        if comm is None:
+            return gather_slabs(slab, n, n, root=0)
+        frame = torch.empty((n, n), dtype=slab.dtype, device=dev) if rank == 0 else None
+        hpdct.gather_rows(comm, slab, frame, n, n, root=0, stream=stream)
+        return frame
+
+    def timed_gather(slab):
+        ms, frame = [], None
         for _ in range(3):
+            frame = None
             barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            full = gather_slabs(y, n, n, root=0)
+            frame = gather(slab)
             torch.cuda.synchronize()
-            gather_ms.append((time.perf_counter() - t0) * 1e3)
-        out["gather_ms"] = round(max_over_ranks(min(gather_ms)), 3)
-        out["gather_bytes_to_root"] = (n * n - rows * n) * 4
-        # int8 wire format (|q| <= 98): forward to int8, gather 1 B/coef, decode on the root
-        y8 = torch.empty((rows, n), dtype=torch.int8, device=dev)
-        hpdct.forward(x, y8)
-        wire_ms = []
-        full8 = None
-        for _ in range(3):
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            g8 = gather_slabs(y8, n, n, root=0)
-            if rank == 0:
-                full8 = g8.float()
-            torch.cuda.synchronize()
-            wire_ms.append((time.perf_counter() - t0) * 1e3)
-        out["gather_int8_ms"] = round(max_over_ranks(min(wire_ms)), 3)
-        if rank == 0:
-            out["int8_wire_equals_fp32"] = bool(torch.equal(full8, full))
-        del y8, full8
-        if rank == 0:
-            # sharded + gathered == the whole frame computed on one GPU
-            xf = torch.empty((n, n), dtype=torch.uint8, device=dev)
-            hpdct.fill_hash_u8(xf, seed=42, first_index=0)
-            ref = hpdct.forward(xf)
-            out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
+            ms.append((time.perf_counter() - t0) * 1e3)
+        return round(max_over_ranks(min(ms)), 3), frame
+
+    out["gather_ms"], full = timed_gather(y)
+    out["gather_bytes_to_root"] = (n * n - rows * n) * 4
+    # int8 wire format (|q| <= 98): forward to int8, gather 1 B/coef, decode on the root
+    y8 = torch.empty((rows, n), dtype=torch.int8, device=dev)
+    hpdct.forward(x, y8)
+    out["gather_int8_ms"], full8 = timed_gather(y8)
+    if rank == 0:
+        out["int8_wire_equals_fp32"] = bool(torch.equal(full8.float(), full))
+    del y8, full8
+    if rank == 0:
+        # sharded + gathered == the whole frame computed on one GPU
+        xf = torch.empty((n, n), dtype=torch.uint8, device=dev)
+        hpdct.fill_hash_u8(xf, seed=42, first_index=0)
+        ref = hpdct.forward(xf)
+        out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
+        del full
+        if world > 1:
             # the same full frame on this one GPU: the compute-phase node speedup
             # (BASELINE.md C4 target >= 6x at 8 GPUs); sets rotated as above
-            del full
             xfs = [xf] + [xf.clone() for _ in range(sets_for(n * n) - 1)]
             refs = [ref] + [torch.empty_like(ref) for _ in range(len(xfs) - 1)]
             fcalls = [hpdct.bind("fwd", a, b, stream=stream) for a, b in zip(xfs, refs)]
             one_gpu_ms = _steady_ms(torch, fcalls, reps, stream)
             out["one_gpu_full_frame_ms"] = round(one_gpu_ms, 4)
             out["compute_speedup_vs_1gpu"] = round(one_gpu_ms / compute_ms, 2)
-            del xf, ref, xfs, refs
-        barrier()
+            del xfs, refs
+        del xf, ref
+    barrier()
+    if comm is not None:
+        comm.destroy()
     del x, y, xs, ys
     torch.cuda.empty_cache()
     return out

@@ -275,8 +275,11 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     return device_status(e, "forward kernel launch");
 }
 
-hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d_coefs, hpdct_dtype out_type,
-                                  int64_t n_frames, int64_t height, int64_t width, void* stream) {
+}  // extern "C"
+
+namespace {
+hpdct_status forward_frames(const uint8_t* const* d_images, void* const* d_coefs, hpdct_dtype out_type,
+                            int64_t n_frames, int64_t height, int64_t width, void* stream) {
     TileGrid g;
     if (hpdct_status st = make_grid(height, width, g)) return st;
     if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "negative frame count");
@@ -304,11 +307,18 @@ hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d
         spans.push_back({i, i + in_bytes, false});
         spans.push_back({o, o + out_bytes, true});
     }
+    // one sweep in start order (O(n log n); input planes may repeat, so a
+    // pairwise scan would be quadratic): a span conflicts if a write span
+    // seen before ends after its start, or if it writes and any span seen
+    // before ends after its start
     std::sort(spans.begin(), spans.end(), [](const Span& x, const Span& y) { return x.a < y.a; });
-    for (size_t k = 0; k < spans.size(); ++k)
-        for (size_t j = k + 1; j < spans.size() && spans[j].a < spans[k].b; ++j)
-            if (spans[k].write || spans[j].write)
-                return fail(HPDCT_ERROR_INVALID_VALUE, "a coefficient plane overlaps another frame's plane");
+    uintptr_t end_all = 0, end_write = 0;
+    for (const Span& sp : spans) {
+        if (sp.a < end_write || (sp.write && sp.a < end_all))
+            return fail(HPDCT_ERROR_INVALID_VALUE, "a coefficient plane overlaps another frame's plane");
+        end_all = std::max(end_all, sp.b);
+        if (sp.write) end_write = std::max(end_write, sp.b);
+    }
     const QState qs = current_qstate();
     if (out_type == HPDCT_I8 && !qs.int8_ok)
         return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
@@ -334,6 +344,22 @@ hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d
         if (e != hipSuccess) return device_status(e, "frame-list forward launch");
     }
     return HPDCT_SUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+// no C++ exception may cross the C ABI: a garbage n_frames makes the span
+// table's allocation throw, which becomes a status here
+hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d_coefs, hpdct_dtype out_type,
+                                  int64_t n_frames, int64_t height, int64_t width, void* stream) {
+    try {
+        return forward_frames(d_images, d_coefs, out_type, n_frames, height, width, stream);
+    } catch (const std::exception& e) {
+        return fail(HPDCT_ERROR_INVALID_VALUE, std::string("hpdct_forward_frames: ") + e.what());
+    } catch (...) {
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_forward_frames: host exception");
+    }
 }
 
 hpdct_status hpdct_inverse(const void* d_coef, hpdct_dtype in_type, void* d_image, hpdct_dtype out_type,

@@ -1,0 +1,194 @@
+// hpdct_dist.cpp -- the row-shard layer of include/hpdct_dist.h on RCCL
+// (libhpdct_dist.so).  The slab kernel is libhpdct's hpdct_forward; the only
+// collective is the gather of the coefficient slabs to the root, as
+// ncclSend / ncclRecv pairs inside one group (rccl.h:700,722), which also
+// covers slabs that differ by a tile row (ncclGather, rccl.h:745, needs equal
+// counts).  Bytes travel as ncclUint8: the element type does not matter to a
+// gather.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "hpdct.h"
+#include "hpdct_dist.h"
+#include "hpdct_kernels.h"
+
+static_assert(HPDCT_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "hpdct_unique_id size");
+
+struct hpdct_comm_s {
+    ncclComm_t nccl;
+    int rank, size, device;
+};
+
+namespace {
+
+hpdct_status fail(hpdct_status st, const std::string& msg) {
+    return static_cast<hpdct_status>(hpdct::set_last_error(st, msg.c_str()));
+}
+hpdct_status nccl_status(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return HPDCT_SUCCESS;
+    return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+hpdct_status hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return HPDCT_SUCCESS;
+    return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+size_t elem_size(hpdct_dtype t) { return t == HPDCT_F32 ? 4 : 1; }
+
+// The caller's current device is restored on scope exit (calls on a
+// communicator run on its device).
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int dev) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// (first_row, rows) of every rank, as hpdct_shard_rows
+void shard(int64_t height, int world, int rank, int64_t& first, int64_t& rows) {
+    const int64_t tile_rows = height / 8, base = tile_rows / world, extra = tile_rows % world;
+    first = (rank * base + (rank < extra ? rank : extra)) * 8;
+    rows = (base + (rank < extra ? 1 : 0)) * 8;
+}
+
+hpdct_status check_geometry(hpdct_comm comm, int64_t height, int64_t width) {
+    if (!comm) return fail(HPDCT_ERROR_INVALID_VALUE, "null communicator");
+    if (height <= 0 || width <= 0 || height % 8 || width % 8)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "height and width must be positive multiples of 8");
+    if (height / 8 < comm->size)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "fewer tile rows (" + std::to_string(height / 8) + ") than ranks (" +
+                                                   std::to_string(comm->size) + ")");
+    return HPDCT_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+hpdct_status hpdct_shard_rows(int64_t height, int world, int rank, int64_t* first_row, int64_t* rows) {
+    if (!first_row || !rows) return fail(HPDCT_ERROR_INVALID_VALUE, "null output pointer");
+    if (height <= 0 || height % 8) return fail(HPDCT_ERROR_INVALID_VALUE, "height must be a positive multiple of 8");
+    if (world < 1 || rank < 0 || rank >= world) return fail(HPDCT_ERROR_INVALID_VALUE, "rank out of range");
+    shard(height, world, rank, *first_row, *rows);
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_comm_init_all(hpdct_comm* comms, int ndev, const int* devices) {
+    if (!comms || !devices || ndev < 1) return fail(HPDCT_ERROR_INVALID_VALUE, "bad communicator list");
+    for (int i = 0; i < ndev; ++i) comms[i] = nullptr;
+    ncclComm_t* raw = new (std::nothrow) ncclComm_t[ndev];
+    if (!raw) return fail(HPDCT_ERROR_DEVICE, "out of host memory");
+    const hpdct_status st = nccl_status(ncclCommInitAll(raw, ndev, devices), "ncclCommInitAll");
+    if (st != HPDCT_SUCCESS) {
+        delete[] raw;
+        return st;
+    }
+    for (int i = 0; i < ndev; ++i) comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i]};
+    delete[] raw;
+    for (int i = 0; i < ndev; ++i)
+        if (!comms[i]) return fail(HPDCT_ERROR_DEVICE, "out of host memory");
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_comm_unique_id(hpdct_unique_id* id) {
+    if (!id) return fail(HPDCT_ERROR_INVALID_VALUE, "null id");
+    ncclUniqueId u;
+    const hpdct_status st = nccl_status(ncclGetUniqueId(&u), "ncclGetUniqueId");
+    if (st == HPDCT_SUCCESS) memcpy(id->internal, u.internal, sizeof(u.internal));
+    return st;
+}
+
+hpdct_status hpdct_comm_init_rank(hpdct_comm* comm, int nranks, const hpdct_unique_id* id, int rank, int device) {
+    if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "bad communicator arguments");
+    *comm = nullptr;
+    DeviceScope ds(device);
+    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    ncclUniqueId u;
+    memcpy(u.internal, id->internal, sizeof(u.internal));
+    ncclComm_t c;
+    if (hpdct_status st = nccl_status(ncclCommInitRank(&c, nranks, u, rank), "ncclCommInitRank")) return st;
+    *comm = new (std::nothrow) hpdct_comm_s{c, rank, nranks, device};
+    if (!*comm) {
+        (void)ncclCommDestroy(c);
+        return fail(HPDCT_ERROR_DEVICE, "out of host memory");
+    }
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_comm_destroy(hpdct_comm comm) {
+    if (!comm) return HPDCT_SUCCESS;
+    const hpdct_status st = nccl_status(ncclCommDestroy(comm->nccl), "ncclCommDestroy");
+    delete comm;
+    return st;
+}
+
+int hpdct_comm_rank(hpdct_comm comm) { return comm ? comm->rank : -1; }
+int hpdct_comm_size(hpdct_comm comm) { return comm ? comm->size : -1; }
+int hpdct_comm_device(hpdct_comm comm) { return comm ? comm->device : -1; }
+
+hpdct_status hpdct_group_start(void) { return nccl_status(ncclGroupStart(), "ncclGroupStart"); }
+hpdct_status hpdct_group_end(void) { return nccl_status(ncclGroupEnd(), "ncclGroupEnd"); }
+
+hpdct_status hpdct_forward_slab(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,
+                                int64_t height, int64_t width, void* stream) {
+    if (hpdct_status st = check_geometry(comm, height, width)) return st;
+    int64_t first, rows;
+    shard(height, comm->size, comm->rank, first, rows);
+    DeviceScope ds(comm->device);
+    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    return hpdct_forward(d_slab, HPDCT_U8, d_coef_slab, out_type, rows, width, nullptr, 0u, stream);
+}
+
+hpdct_status hpdct_gather_rows(hpdct_comm comm, const void* d_slab, void* d_frame, hpdct_dtype type, int64_t height,
+                               int64_t width, int root, void* stream) {
+    if (hpdct_status st = check_geometry(comm, height, width)) return st;
+    if (type != HPDCT_F32 && type != HPDCT_I8 && type != HPDCT_U8)
+        return fail(HPDCT_ERROR_UNSUPPORTED, "gather type must be HPDCT_F32, HPDCT_I8 or HPDCT_U8");
+    if (root < 0 || root >= comm->size) return fail(HPDCT_ERROR_INVALID_VALUE, "root out of range");
+    if (!d_slab) return fail(HPDCT_ERROR_INVALID_VALUE, "null slab pointer");
+    if (comm->rank == root && !d_frame) return fail(HPDCT_ERROR_INVALID_VALUE, "null frame pointer on the root");
+    const size_t row_bytes = static_cast<size_t>(width) * elem_size(type);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DeviceScope ds(comm->device);
+    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    int64_t first, rows;
+    if (comm->rank != root) {
+        shard(height, comm->size, comm->rank, first, rows);
+        return nccl_status(ncclSend(d_slab, static_cast<size_t>(rows) * row_bytes, ncclUint8, root, comm->nccl, s),
+                           "ncclSend");
+    }
+    char* frame = static_cast<char*>(d_frame);
+    if (hpdct_status st = nccl_status(ncclGroupStart(), "ncclGroupStart")) return st;
+    hpdct_status st = HPDCT_SUCCESS;
+    for (int r = 0; r < comm->size && st == HPDCT_SUCCESS; ++r) {
+        shard(height, comm->size, r, first, rows);
+        char* dst = frame + static_cast<size_t>(first) * row_bytes;
+        const size_t bytes = static_cast<size_t>(rows) * row_bytes;
+        if (r == root) {
+            if (dst != d_slab)
+                st = hip_status(hipMemcpyAsync(dst, d_slab, bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+        } else {
+            st = nccl_status(ncclRecv(dst, bytes, ncclUint8, r, comm->nccl, s), "ncclRecv");
+        }
+    }
+    const hpdct_status end = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    return st != HPDCT_SUCCESS ? st : end;
+}
+
+hpdct_status hpdct_forward_sharded(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,
+                                   void* d_frame, int64_t height, int64_t width, int root, void* stream) {
+    if (hpdct_status st = hpdct_forward_slab(comm, d_slab, d_coef_slab, out_type, height, width, stream)) return st;
+    return hpdct_gather_rows(comm, d_coef_slab, d_frame, out_type, height, width, root, stream);
+}
+
+}  // extern "C"

@@ -20,7 +20,9 @@
 //   sse_u8  = sum (x - u8(R+128))^2        pixel bytes (x.x, x.r8, r8.r8), uint64
 //   sse_f32 = sum (x - (R+128))^2          per tile an fp32 fma chain over the 64
 //             pixels, rounded to a multiple of 2^-16 and added as uint64: the
-//             result does not depend on the order tiles finish in.
+//             result does not depend on the order tiles finish in, but it is
+//             not the exact sum (each tile's fp32 chain rounds; relative error
+//             ~1e-9 at 8192^2, tests/test_gpu_roundtrip.py)
 // Workgroup partials are added with one 64-bit atomic per field per workgroup.
 #pragma once
 
@@ -29,6 +31,9 @@
 namespace hpdct {
 
 constexpr float kRtFixScale = 65536.0f;  // sse_f32 fixed point: 2^-16
+// bit 63 of sse_f32_fx: some tile's sse_f32 was non-finite or >= 2^24 (the
+// field then holds no sum; include/hpdct.h HPDCT_SSE_F32_INVALID)
+constexpr unsigned long long kRtSseF32Invalid = 1ull << 63;
 
 namespace {
 
@@ -60,12 +65,11 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // profiles/r01/mappings/kbench2_rt.log)
 template <int kRecon>
 constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
-// kWaveAtomics: each wave adds its partials with its own 64-bit atomics (no
-// workgroup barrier in the epilogue); false: one atomic per field per workgroup
-// kSpreadSums (diagnostic): workgroup b adds into sums[b] instead of sums[0]
-// (the caller passes one RtSums per workgroup), to price the same-line atomics
-template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false, bool kWaveAtomics = false,
-          bool kSpreadSums = false>
+// Epilogue: one 64-bit atomic add per field per workgroup into the caller's
+// struct.  Measured alternatives (round 3, profiles/r03/kb_rt16.log, 8192^2):
+// one struct per workgroup (no two workgroups on one line) 78.4-78.8 us
+// against 79.7 us; per-wave atomics 607 us.
+template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false>
 __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
@@ -177,32 +181,33 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
     });
 
     if constexpr (kStats) {
-        // lanes without a tile (ragged last set, or waves past the end) hold zeros
-        // < 2^24 * 2^16 for any finite reconstruction: exact in the convert; a
-        // non-finite one (IEEE path, extreme table) saturates the field
+        // lanes without a tile (ragged last set, or waves past the end) hold zeros.
+        // A tile's fixed-point sse_f32 below 2^40 (sse < 2^24, i.e. a mean
+        // |x - R| under 512 per pixel) is added exactly; a larger or non-finite
+        // one (IEEE path with an extreme table) adds nothing and sets the
+        // sticky bit 63 of the field instead (kRtSseF32Invalid): the sum can
+        // then neither wrap nor read as a small value
         const float fx = __builtin_rintf(acc_f * kRtFixScale);
-        unsigned long long f = fx < 1.8e19f ? static_cast<unsigned long long>(fx) : ~0ull >> 8;
+        const bool f_ok = fx < 0x1p40f;  // false for NaN
+        unsigned long long f = f_ok ? static_cast<unsigned long long>(fx) : 0ull;
         unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
         unsigned long long xx = static_cast<unsigned long long>(acc_xx);
         f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
-        if constexpr (kWaveAtomics) {
-            if (lane == 0u) {
-                auto* out = reinterpret_cast<unsigned long long*>(sums);
-                if (f) atomicAdd(out + 0, f);
-                if (e8) atomicAdd(out + 1, e8);
-                if (xx) atomicAdd(out + 2, xx);
-            }
-            return;
-        }
+        // a wave's f is < 64 * 2^40: bit 63 of its slot carries the wave's flag
+        if (__builtin_amdgcn_ballot_w64(!f_ok) != 0) f |= kRtSseF32Invalid;
         __shared__ unsigned long long part[512 / 64][3];
         const uint32_t w = threadIdx.x / 64u;
         if ((threadIdx.x & 63u) == 0u) part[w][0] = f, part[w][1] = e8, part[w][2] = xx;
         __syncthreads();
         if (threadIdx.x < 3u) {
-            unsigned long long s = 0;
-            for (uint32_t k = 0; k < 512u / 64u; ++k) s += part[k][threadIdx.x];
-            RtSums* const dst = kSpreadSums ? sums + blockIdx.x : sums;
-            if (s) atomicAdd(reinterpret_cast<unsigned long long*>(dst) + threadIdx.x, s);
+            unsigned long long s = 0, bad = 0;
+            for (uint32_t k = 0; k < 512u / 64u; ++k) {
+                s += part[k][threadIdx.x] & ~kRtSseF32Invalid;
+                bad |= part[k][threadIdx.x] & kRtSseF32Invalid;
+            }
+            auto* const dst = reinterpret_cast<unsigned long long*>(sums) + threadIdx.x;
+            if (s) atomicAdd(dst, s);
+            if (bad) atomicOr(dst, kRtSseF32Invalid);
         }
     }
 }

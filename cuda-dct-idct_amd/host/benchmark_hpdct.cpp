@@ -8,9 +8,14 @@
 // whole sequence (image re-uploaded each time, since the forward leaves X-128
 // in it) to average warm calls; the first call of a process includes loading
 // the kernels' code object.
+//
+// `benchmark_hpdct <n> [runs] --gpus N [--int8]` is the build's own C4 mode
+// (shard_bench.hpp): the n x n frame row-sharded over N GPUs of this process,
+// RCCL gather to device 0 (include/hpdct_dist.h).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "hpdct_compat.h"
 
@@ -23,13 +28,32 @@
         }                                                             \
     }
 
+#include "shard_bench.hpp"
+
 int main(int argc, char* argv[]) {
-    if (argc != 2 && argc != 3) {
-        printf("Use: %s <width/height> [runs]\n", argv[0]);
+    // options of the sharded mode, anywhere after the size
+    int gpus = 0;
+    bool int8 = false;
+    int npos = 0;
+    char* pos[2] = {NULL, NULL};
+    for (int i = 1; i < argc; ++i) {
+        if (strcmp(argv[i], "--gpus") == 0 && i + 1 < argc) {
+            gpus = atoi(argv[++i]);
+        } else if (strcmp(argv[i], "--int8") == 0) {
+            int8 = true;
+        } else if (npos < 2) {
+            pos[npos++] = argv[i];
+        } else {
+            npos = 3;
+        }
+    }
+    if (npos != 1 && npos != 2) {
+        printf("Use: %s <width/height> [runs] [--gpus N [--int8]]\n", argv[0]);
         return 1;
     }
-    const size_t n = strtoul(argv[1], NULL, 10);
-    const long runs = argc == 3 ? strtol(argv[2], NULL, 10) : 1;
+    const size_t n = strtoul(pos[0], NULL, 10);
+    const long runs = npos == 2 ? strtol(pos[1], NULL, 10) : 1;
+    if (gpus > 0) return run_sharded(n, gpus, int8, runs);
     const size_t width = n, height = n;
     const size_t px = width * height;
 

@@ -336,6 +336,7 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
 
 
 SSE_F32_UNIT = 1.0 / 65536.0  # HPDCT_SSE_F32_UNIT
+SSE_F32_INVALID = 1 << 63     # HPDCT_SSE_F32_INVALID
 
 
 def _roundtrip_args(image, coef, recon, sums_buf, height, width, stream):
@@ -357,7 +358,10 @@ def sums_from_buffer(sums_buf) -> dict:
     """The 3 x uint64 device struct hpdct_roundtrip_sums (held in an int64
     tensor) as {"sse_f32", "sse_u8", "sum_x2"} (synchronises)."""
     v = [int(x) & ((1 << 64) - 1) for x in sums_buf.cpu().tolist()]
-    return {"sse_f32": v[0] * SSE_F32_UNIT, "sse_u8": v[1], "sum_x2": v[2]}
+    # bit 63: some tile's fp32 error sum was non-finite or too large to add
+    # (HPDCT_SSE_F32_INVALID): no finite sse_f32 exists for the frame
+    sse_f32 = float("inf") if v[0] & SSE_F32_INVALID else v[0] * SSE_F32_UNIT
+    return {"sse_f32": sse_f32, "sse_u8": v[1], "sum_x2": v[2]}
 
 
 def quality_from_sums(sums: dict, pixels: int) -> dict:
@@ -588,3 +592,143 @@ def convert_to_unsigned_char(a: np.ndarray) -> np.ndarray:
     o = np.empty(a.shape, np.uint8)
     load_library().hpdct_f32_to_u8(a.ctypes.data, o.ctypes.data, a.size)
     return o
+
+
+# ---------------------------------------------------------------------------
+# row-shard layer over RCCL (include/hpdct_dist.h, lib/libhpdct_dist.so):
+# BASELINE config C4.  The reference has no multi-GPU code.
+# ---------------------------------------------------------------------------
+DIST_LIB_PATH = os.environ.get("HPDCT_DIST_LIB", os.path.join(_HERE, "lib", "libhpdct_dist.so"))
+DIST_SYMBOLS = [
+    "hpdct_shard_rows", "hpdct_comm_init_all", "hpdct_comm_unique_id", "hpdct_comm_init_rank",
+    "hpdct_comm_destroy", "hpdct_comm_rank", "hpdct_comm_size", "hpdct_comm_device",
+    "hpdct_group_start", "hpdct_group_end", "hpdct_forward_slab", "hpdct_gather_rows", "hpdct_forward_sharded",
+]
+UNIQUE_ID_BYTES = 128
+_dist = None
+
+
+def load_dist_library() -> ctypes.CDLL:
+    """Load (once) libhpdct_dist.so; it needs librccl.so.1 (inside a torch
+    process that is torch's own RCCL, already loaded under the same soname)."""
+    global _dist
+    if _dist is not None:
+        return _dist
+    load_library()
+    if not os.path.exists(DIST_LIB_PATH):
+        raise HpdctLibraryError(f"{DIST_LIB_PATH} not found: build it with `make -C cuda-dct-idct_amd`")
+    try:
+        lib = ctypes.CDLL(DIST_LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the loader
+        raise HpdctLibraryError(f"cannot load {DIST_LIB_PATH}: {e}") from e
+    vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    lib.hpdct_shard_rows.argtypes = [i64, ci, ci, vp, vp]
+    lib.hpdct_comm_init_all.argtypes = [vp, ci, vp]
+    lib.hpdct_comm_unique_id.argtypes = [vp]
+    lib.hpdct_comm_init_rank.argtypes = [vp, ci, vp, ci, ci]
+    lib.hpdct_comm_destroy.argtypes = [vp]
+    for f in (lib.hpdct_comm_rank, lib.hpdct_comm_size, lib.hpdct_comm_device):
+        f.argtypes = [vp]
+        f.restype = ci
+    lib.hpdct_group_start.argtypes = []
+    lib.hpdct_group_end.argtypes = []
+    lib.hpdct_forward_slab.argtypes = [vp, vp, vp, ci, i64, i64, vp]
+    lib.hpdct_gather_rows.argtypes = [vp, vp, vp, ci, i64, i64, ci, vp]
+    lib.hpdct_forward_sharded.argtypes = [vp, vp, vp, ci, vp, i64, i64, ci, vp]
+    for name in DIST_SYMBOLS:
+        if name not in ("hpdct_comm_rank", "hpdct_comm_size", "hpdct_comm_device"):
+            getattr(lib, name).restype = ci
+    _dist = lib
+    return lib
+
+
+def shard_rows_native(height: int, world: int, rank: int):
+    """(first_row, rows) of `rank` from the C-ABI (hpdct_shard_rows)."""
+    first, rows = ctypes.c_int64(), ctypes.c_int64()
+    _check(load_dist_library().hpdct_shard_rows(int(height), int(world), int(rank), ctypes.byref(first),
+                                                ctypes.byref(rows)))
+    return first.value, rows.value
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (rank 0 creates it, the caller hands it to every rank)."""
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(load_dist_library().hpdct_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """An RCCL communicator of the row-shard layer (hpdct_comm)."""
+
+    def __init__(self, handle: int):
+        self.handle = ctypes.c_void_p(handle)
+
+    @classmethod
+    def init_all(cls, devices):
+        """One communicator per device of this process (ncclCommInitAll)."""
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        hs = (ctypes.c_void_p * len(devices))()
+        _check(load_dist_library().hpdct_comm_init_all(hs, len(devices), devs))
+        return [cls(h) for h in hs]
+
+    @classmethod
+    def init_rank(cls, nranks: int, unique_id: bytes, rank: int, device: int):
+        """One communicator per process (ncclCommInitRank on `device`)."""
+        if len(unique_id) != UNIQUE_ID_BYTES:
+            raise HpdctError(1, f"unique id must be {UNIQUE_ID_BYTES} bytes")
+        h = ctypes.c_void_p()
+        uid = ctypes.create_string_buffer(bytes(unique_id), UNIQUE_ID_BYTES)
+        _check(load_dist_library().hpdct_comm_init_rank(ctypes.byref(h), int(nranks), uid, int(rank), int(device)))
+        return cls(h.value)
+
+    @property
+    def rank(self) -> int:
+        return load_dist_library().hpdct_comm_rank(self.handle)
+
+    @property
+    def size(self) -> int:
+        return load_dist_library().hpdct_comm_size(self.handle)
+
+    @property
+    def device(self) -> int:
+        return load_dist_library().hpdct_comm_device(self.handle)
+
+    def destroy(self) -> None:
+        if self.handle:
+            _check(load_dist_library().hpdct_comm_destroy(self.handle))
+            self.handle = ctypes.c_void_p()
+
+
+def group_start() -> None:
+    _check(load_dist_library().hpdct_group_start())
+
+
+def group_end() -> None:
+    _check(load_dist_library().hpdct_group_end())
+
+
+def forward_slab(comm: Comm, slab, coef_slab, height: int, width: int, stream=None) -> None:
+    """The fused forward kernel on this rank's slab (hpdct_forward_slab):
+    slab = rows x width uint8 of the height x width frame, rows from
+    shard_rows_native(height, comm.size, comm.rank)."""
+    torch = _torch()
+    _, rows = shard_rows_native(height, comm.size, comm.rank)
+    _device_plane(slab, "slab", None, rows * width, (torch.uint8,))
+    _device_plane(coef_slab, "coefficient slab", slab.device, rows * width, (torch.float32, torch.int8))
+    _check(load_dist_library().hpdct_forward_slab(comm.handle, ctypes.c_void_p(slab.data_ptr()),
+                                                  ctypes.c_void_p(coef_slab.data_ptr()), _dtype_code(coef_slab),
+                                                  int(height), int(width), _stream_ptr(stream)))
+
+
+def gather_rows(comm: Comm, slab, frame, height: int, width: int, root: int = 0, stream=None) -> None:
+    """Every rank's slab to the root's height x width `frame` over RCCL
+    (hpdct_gather_rows); `frame` is ignored (may be None) off the root."""
+    _, rows = shard_rows_native(height, comm.size, comm.rank)
+    _device_plane(slab, "slab", None, rows * width)
+    fp = None
+    if comm.rank == root:
+        _device_plane(frame, "frame", slab.device, int(height) * int(width), (slab.dtype,))
+        fp = ctypes.c_void_p(frame.data_ptr())
+    _check(load_dist_library().hpdct_gather_rows(comm.handle, ctypes.c_void_p(slab.data_ptr()), fp,
+                                                 _dtype_code(slab), int(height), int(width), int(root),
+                                                 _stream_ptr(stream)))

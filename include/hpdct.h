@@ -141,12 +141,17 @@ hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t 
  * PEEN = 100 sqrt(sse / sum_x2) %, MSE = sse / (height*width) (the
  * definitions of the README table). */
 typedef struct hpdct_roundtrip_sums {
-    uint64_t sse_f32_fx; /* sum (x - (R+128))^2 in units of 2^-16 (HPDCT_SSE_F32_UNIT): per-tile fp32
-                            partial sums, each rounded to the unit, added exactly */
+    uint64_t sse_f32_fx; /* sum (x - (R+128))^2 in units of 2^-16 (HPDCT_SSE_F32_UNIT): each tile's
+                            fp32 partial sum (an fma chain over its 64 pixels, so NOT the exact sum:
+                            relative error ~1e-9 on a 8192^2 frame) rounded to the unit, the tiles
+                            then added exactly in any order.  Bit 63 (HPDCT_SSE_F32_INVALID) is set,
+                            sticky, when some tile's partial sum is non-finite or >= 2^24 (an
+                            extreme caller table on the IEEE path): the field then holds no sum */
     uint64_t sse_u8;     /* sum (x - u8(R+128))^2, exact */
     uint64_t sum_x2;     /* sum x^2, exact */
 } hpdct_roundtrip_sums;
 #define HPDCT_SSE_F32_UNIT (1.0 / 65536.0)
+#define HPDCT_SSE_F32_INVALID (1ull << 63)
 hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_recon, hpdct_dtype recon_type,
                                 hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream);
 

@@ -12,16 +12,21 @@ import re
 import subprocess
 
 import numpy as np
+import time
+
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INCLUDE = os.path.join(ROOT, "include")
 
 
-def header_functions():
+DIST_HEADER = "hpdct_dist.h"  # declares libhpdct_dist.so (the RCCL row-shard layer), not libhpdct.so
+
+
+def header_functions(only=None):
     names = set()
     for fn in os.listdir(INCLUDE):
-        if not fn.endswith(".h"):
+        if not fn.endswith(".h") or (fn == DIST_HEADER) != (only == DIST_HEADER):
             continue
         text = open(os.path.join(INCLUDE, fn)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
@@ -46,6 +51,15 @@ def test_library_exports_every_declared_symbol(hp):
         else:
             assert name in syms, name
     assert set(hp.C_SYMBOLS) | set(hp.COMPAT_SYMBOLS) == declared
+
+
+def test_dist_library_exports_every_declared_symbol(hp):
+    declared = header_functions(only=DIST_HEADER)
+    assert {"hpdct_gather_rows", "hpdct_forward_slab", "hpdct_comm_init_all"} <= declared
+    syms = exported_symbols(hp.DIST_LIB_PATH)
+    for name in declared:
+        assert name in syms, name
+    assert set(hp.DIST_SYMBOLS) == declared
 
 
 def test_compat_mangling_matches_reference_signatures(tmp_path):
@@ -264,6 +278,19 @@ def test_forward_frames_arguments_rejected(hp):
         assert ff(ins, outs, hp.I8, 3, 64, 64, None) == 3  # int8 overflow with this table
     finally:
         hp.set_quant_table(None)
+    # a garbage count: the span table cannot be allocated; a status, not an
+    # exception across the C ABI (std::terminate)
+    assert ff(ins, outs, hp.F32, 1 << 62, 64, 64, None) == 1
+    assert b"hpdct_forward_frames" in L.hpdct_last_error_string()
+    # a large list from a small repeated pool: the overlap sweep is O(n log n)
+    n = 20000
+    many_in = (ctypes.c_void_p * n)(*[(1 << 20) + (k % 4) * (1 << 16) for k in range(n)])
+    many_out = (ctypes.c_void_p * n)(*[(1 << 32) + k * (1 << 16) for k in range(n)])
+    many_out[n - 1] = (1 << 20) + 8  # the last plane lands on a pool input
+    t0 = time.perf_counter()
+    assert ff(many_in, many_out, hp.I8, n, 64, 64, None) == 1
+    assert time.perf_counter() - t0 < 1.0
+    assert b"overlap" in L.hpdct_last_error_string()
 
 
 def test_host_rand_matches_glibc(hp, oracle):

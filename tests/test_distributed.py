@@ -89,3 +89,34 @@ def test_sharded_gather_equals_unsharded(tmp_path, world, height, width, wire):
     result = tmp_path / "result.txt"
     mp.spawn(_worker, args=(world, _free_port(), height, width, str(result), wire), nprocs=world, join=True)
     assert result.read_text() == "ok"
+
+
+# ---- the native row-shard layer (include/hpdct_dist.h, libhpdct_dist.so) ----
+# Host-only parts run here: the library loads (with librccl) and exports
+# every declared symbol, its partition equals hpdct_dist.shard_rows, and bad
+# arguments are rejected before any device work.  The RCCL gather itself
+# runs in tests/test_gpu_dist.py.
+
+
+
+
+@pytest.mark.parametrize("height,world", [(8, 1), (64, 2), (72, 2), (16384, 8), (8192, 3), (40, 8), (800, 7)])
+def test_native_shard_rows_equals_python(height, world):
+    import hpdct
+    for r in range(world):
+        assert hpdct.shard_rows_native(height, world, r) == shard_rows(height, world, r)
+
+
+def test_native_dist_rejects_bad_arguments():
+    import hpdct
+    for h, w, r in ((12, 2, 0), (0, 1, 0), (16, 2, 2), (16, 0, 0), (16, 2, -1)):
+        with pytest.raises(hpdct.HpdctError):
+            hpdct.shard_rows_native(h, w, r)
+    lib = hpdct.load_dist_library()
+    # null communicator: refused with a status, no device touched
+    assert lib.hpdct_gather_rows(None, None, None, 2, 64, 64, 0, None) == 1
+    assert lib.hpdct_forward_slab(None, None, None, 2, 64, 64, None) == 1
+    assert lib.hpdct_comm_rank(None) == -1 and lib.hpdct_comm_size(None) == -1
+    assert lib.hpdct_comm_destroy(None) == 0
+    with pytest.raises(hpdct.HpdctError):
+        hpdct.Comm.init_rank(1, b"x" * 10, 0, 0)

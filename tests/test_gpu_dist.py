@@ -1,0 +1,124 @@
+"""The native row-shard layer over RCCL (include/hpdct_dist.h,
+libhpdct_dist.so) on the GPU, at world size 1 (the GPU box has one MI355X):
+
+  - a communicator from ncclCommInitAll and one from a unique id +
+    ncclCommInitRank;
+  - hpdct_forward_slab + hpdct_gather_rows of fp32 and int8 coefficients and
+    of uint8 pixels, bit-exact against hpdct_forward of the whole frame (at
+    world 1 the root's slab is the frame: the gather copies it device to
+    device into the root's frame buffer);
+  - the single-process multi-device driver `benchmark_hpdct <n> --gpus 1`
+    (ncclCommInitAll, slab forward, RCCL gather, byte compare);
+  - bench.py's process-group path at WORLD_SIZE=1 (init_process_group("nccl"),
+    device-tensor all_reduce) with its C4 leg on the native gather.
+
+The world-size >= 2 flow of the same partition runs over gloo on the CPU
+(tests/test_distributed.py) and with the HIP kernel in two processes on one
+GPU (tests/test_gpu_configs.py); RCCL ranks need a GPU each.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def comm1(hp, dev):
+    c = hp.Comm.init_all([dev.index])[0]
+    assert (c.rank, c.size, c.device) == (0, 1, dev.index)
+    yield c
+    c.destroy()
+
+
+@pytest.mark.parametrize("out_dtype", ["float32", "int8"])
+@pytest.mark.parametrize("h,w", [(2048, 4096), (1032, 520)])
+def test_world1_slab_forward_and_gather_equal_forward(hp, dev, comm1, out_dtype, h, w):
+    import torch
+    x = torch.empty((h, w), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=11)
+    dt = getattr(torch, out_dtype)
+    slab = torch.empty((h, w), dtype=dt, device=dev)
+    frame = torch.full((h, w), 3, dtype=dt, device=dev)
+    hp.forward_slab(comm1, x, slab, h, w)
+    hp.gather_rows(comm1, slab, frame, h, w, root=0)
+    ref = hp.forward(x, out_dtype=dt)
+    torch.cuda.synchronize()
+    if dt == torch.float32:
+        assert torch.equal(slab.view(torch.int32), ref.view(torch.int32))
+        assert torch.equal(frame.view(torch.int32), ref.view(torch.int32))
+    else:
+        assert torch.equal(slab, ref) and torch.equal(frame, ref)
+
+
+def test_world1_gather_uint8_pixels(hp, dev, comm1):
+    import torch
+    x = torch.randint(0, 256, (64, 128), dtype=torch.uint8, device=dev)
+    frame = torch.zeros_like(x)
+    hp.gather_rows(comm1, x, frame, 64, 128, root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, x)
+
+
+def test_world1_comm_from_unique_id(hp, dev):
+    import torch
+    uid = hp.comm_unique_id()
+    assert len(uid) == hp.UNIQUE_ID_BYTES
+    c = hp.Comm.init_rank(1, uid, 0, dev.index)
+    try:
+        x = torch.empty((512, 1024), dtype=torch.uint8, device=dev)
+        hp.fill_hash_u8(x, seed=3)
+        slab = torch.empty((512, 1024), dtype=torch.float32, device=dev)
+        frame = torch.empty_like(slab)
+        hp.forward_slab(c, x, slab, 512, 1024)
+        hp.gather_rows(c, slab, frame, 512, 1024, root=0)
+        torch.cuda.synchronize()
+        assert torch.equal(frame.view(torch.int32), hp.forward(x).view(torch.int32))
+    finally:
+        c.destroy()
+
+
+def test_world1_gather_rejects_bad_root(hp, dev, comm1):
+    import torch
+    s = torch.empty((64, 64), dtype=torch.float32, device=dev)
+    with pytest.raises(hp.HpdctError):
+        hp.gather_rows(comm1, s, s.clone(), 64, 64, root=1)
+
+
+def test_driver_sharded_mode_one_gpu():
+    exe = os.path.join(ROOT, "cuda-dct-idct_amd", "bin", "benchmark_hpdct")
+    r = subprocess.run([exe, "4096", "3", "--gpus", "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bit-exact yes" in r.stdout, r.stdout
+    r = subprocess.run([exe, "2048", "--gpus", "1", "--int8"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "int8" in r.stdout and "bit-exact yes" in r.stdout, r.stdout + r.stderr
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_nccl_process_group_at_world_size_1(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5", "--warmup", "2",
+           "--size", "2048", "--sets", "4", "--no-cpu-baseline", "--sustain-s", "0", "--c4-size", "2048",
+           "--c5-size", "512", "--c5-frames", "8"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c4 = line["extras"]["c4"]
+    assert c4["gather_path"].startswith("native RCCL"), c4
+    assert c4["sharded_equals_unsharded"] is True
+    assert c4["int8_wire_equals_fp32"] is True
+    assert line["parity_spot_check"] is True

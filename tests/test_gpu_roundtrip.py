@@ -221,6 +221,10 @@ def test_roundtrip_extreme_quant_table(hp, oracle, dev, tiny):
     assert nan_aware_bits_equal(to_host(recf), r)
     assert nan_aware_bits_equal(to_host(two), r)
     assert got["sum_x2"] == sums["sum_x2"] and got["sse_u8"] == sums["sse_u8"]
+    # NaN reconstructions: the fp32 error sum has no finite value, and the
+    # device says so (sticky HPDCT_SSE_F32_INVALID -> inf), it never reads as
+    # a small number (the field used to wrap modulo 2^64)
+    assert not np.isfinite(sums["sse_f32"]) and got["sse_f32"] == float("inf")
 
 
 def test_roundtrip_extremes(hp, oracle, dev):

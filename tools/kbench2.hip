@@ -33,6 +33,7 @@
 #include "kbench_mfma.hpp"
 #include "hpdct_roundtrip.hpp"
 #include "kbench_linread.hpp"
+#include "kbench_dma.hpp"
 
 using namespace hpdct;
 
@@ -156,6 +157,17 @@ void lin_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     lin::linread_go<kVarFastDiv>(static_cast<const uint8_t*>(in), static_cast<float*>(out), c.g, c.qp, s);
 }
 
+// linear input reads through an LDS-DMA double buffer, persistent workgroups (kbench_dma.hpp)
+template <uint32_t kWaves, uint32_t kWgsPerCu>
+void dma_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (!dma::dma_ok<kWaves>(c.g)) {
+        fprintf(stderr, "dma: width must be a multiple of %u px\n", kWaves * 512u);
+        exit(2);
+    }
+    (void)dma::dma_go<kVarFastDiv, kWaves>(static_cast<const uint8_t*>(in), static_cast<float*>(out), c.g, c.qp, c.cus,
+                                           kWgsPerCu, s);
+}
+
 template <bool kFast>
 void mfma_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     (void)hpdct::fdct_mfma_i8_go<kFast>(static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), c.g, c.qp, s);
@@ -186,17 +198,10 @@ void rt_fused(const void* in, void* out, const Ctx& c, hipStream_t s) {
                      kRecon, kStats ? g_sums : nullptr, c.g, c.qp, kFast, s, true);
 }
 
-// one RtSums per workgroup (diagnostic: no two workgroups add into one line)
-void rt_spread(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    static RtSums* spread = nullptr;
-    if (!spread) (void)hipMalloc(&spread, sizeof(RtSums) * roundtrip_grid(c.g).x);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, 2, false, false, true>), roundtrip_grid(c.g),
-                       dim3(512), 0, s, static_cast<const uint8_t*>(in), g_coef2[set_of(in)], out, spread, c.g, c.qp);
-}
-template <int kRaw, bool kWave = false, bool kMemset = true>
+template <int kRaw, bool kMemset = true>
 void rt_raw(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kMemset) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw, false, kWave>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw, false>), roundtrip_grid(c.g), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef2[set_of(in)], out, g_sums, c.g, c.qp);
 }
 
@@ -288,11 +293,8 @@ int main(int argc, char** argv) {
         {"rt", "rt fused u8 recon + sums, raw in VGPRs", rt_raw<0>, true},
         {"rt", "rt fused u8 recon + sums, raw re-read", rt_raw<1>, true},
         {"rt", "rt fused u8 recon + sums, raw in LDS", rt_raw<2>, true},
-        {"rt", "rt sums, no memset (accumulate)", rt_raw<2, false, false>, true},
-        {"rt", "rt sums, no memset, one RtSums per workgroup", rt_spread, true},
-        {"rt", "rt sums, no memset (accumulate) again", rt_raw<2, false, false>, true},
-        {"rt", "rt sums, no memset, one RtSums per workgroup again", rt_spread, true},
-        {"rt", "rt fused u8 recon + sums, per-wave atomics", rt_raw<2, true>, true},
+        {"rt", "rt sums, no memset (accumulate)", rt_raw<2, false>, true},
+        {"rt", "rt sums, no memset (accumulate) again", rt_raw<2, false>, true},
         {"rt", "rt fused u8 recon + sums, raw in LDS again", rt_raw<2>, true},
         {"rt", "rt fused sums only (5 B/px)", rt_fused<kRtReconNone, true, true>, false},
         {"rt", "rt fused f32 recon + sums (9 B/px)", rt_fused<kRtReconF32, true, true>, false},
@@ -324,6 +326,16 @@ int main(int argc, char** argv) {
         {"lin", "fwd u8->f32 library b1024", prod_f32_fwd<(kProdVar<uint8_t, float> & ~(3u << 12)) | W1024 | F>, true},
         {"lin", "fwd u8->f32 library (b512) again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
         {"lin", "fwd u8->f32 linear reads via LDS again", lin_f32_fwd, true},
+        // linear reads through an LDS-DMA double buffer (kbench_dma.hpp): waves per workgroup x workgroups per CU
+        {"dma", "fwd u8->f32 library (b512)", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"dma", "fwd u8->f32 dma 8w x 2/cu", dma_f32_fwd<8, 2>, true},
+        {"dma", "fwd u8->f32 dma 8w x 1/cu", dma_f32_fwd<8, 1>, true},
+        {"dma", "fwd u8->f32 dma 4w x 4/cu", dma_f32_fwd<4, 4>, true},
+        {"dma", "fwd u8->f32 dma 4w x 2/cu", dma_f32_fwd<4, 2>, true},
+        {"dma", "fwd u8->f32 dma 16w x 1/cu", dma_f32_fwd<16, 1>, true},
+        {"dma", "fwd u8->f32 dma 8w not persistent", dma_f32_fwd<8, 64>, true},
+        {"dma", "fwd u8->f32 library (b512) again", prod_f32_fwd<kProdVar<uint8_t, float> | F>, true},
+        {"dma", "fwd u8->f32 dma 8w x 2/cu again", dma_f32_fwd<8, 2>, true},
         // copysign as v_bitop3_b32 (library) against v_bfi_b32 (the ab:: copy)
         {"b3", "fwd u8->i8 ab copy (bfi)", i8_fwd<I8>, true},
         {"b3", "fwd u8->i8 library (bitop3)", prod_i8_fwd<I8>, true},
@@ -348,7 +360,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> ref(px * 4), got(px * 4);
         std::string cur;
         for (auto& v : vars) {
-            const size_t nb = v.group == "wide" || v.group == "tlb" || v.group == "b3f" || v.group == "lin" ? px * 4 : px;  // fp32 output plane
+            const size_t nb = v.group == "wide" || v.group == "tlb" || v.group == "b3f" || v.group == "lin" || v.group == "dma" ? px * 4 : px;  // fp32 output plane
             CK(hipMemset(out[2], 0xa5, nb));
             v.launch(src(v, 1), out[2], c, 0);
             const hipError_t le = hipGetLastError();
@@ -435,7 +447,7 @@ int main(int argc, char** argv) {
         if (t.empty()) continue;
         std::sort(t.begin(), t.end());
         const double med = t[t.size() / 2];
-        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" || vars[v].group == "b3f" || vars[v].group == "lin" ? 5.0 : 2.0;
+        double bpp = vars[v].group == "inv" || vars[v].group == "wide" || vars[v].group == "tlb" || vars[v].group == "b3f" || vars[v].group == "lin" || vars[v].group == "dma" ? 5.0 : 2.0;
         if (vars[v].group == "rt") {
             const std::string& nm = vars[v].name;
             bpp = nm.find("(10 B") != std::string::npos  ? 10.0

@@ -1,0 +1,267 @@
+// kbench3.hip -- lean A/B bench for the round-3 kernel work (fast to build:
+// only the library headers and the variants under test, not the whole
+// variant zoo of kbench2).  One HxW uint8 frame per buffer set, sets rotated
+// (16 sets at 8192^2 = 1 GiB of inputs, 4x the Infinity Cache), interleaved
+// rounds, median of per-batch averages, every variant checked bit-for-bit
+// against its group's first entry before timing.
+//
+//   kbench3 [n=8192 | HxW] [iters=64] [rounds=3] [group=all|fwd] [sets=16]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "hpdct_launch.hpp"
+#include "kbench_dma.hpp"
+#include "kbench_band.hpp"
+
+using namespace hpdct;
+
+int hpdct::mapping_mode() { return 0; }
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));       \
+            exit(2);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+struct Ctx {
+    TileGrid g;
+    QParams qp;
+    uint32_t cus;
+};
+typedef void (*LaunchFn)(const void* in, void* out, const Ctx& c, hipStream_t s);
+struct Variant {
+    std::string group, name;
+    LaunchFn launch;
+    double bpp;    // algorithmic bytes per pixel
+    size_t obpp;   // output plane bytes per pixel (the check compares this plane)
+    bool check;
+};
+
+template <unsigned kVar>
+void prod_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, float, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+template <uint32_t kWaves, uint32_t kWgsPerCu>
+void dma_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (!dma::dma_ok<kWaves>(c.g)) {
+        fprintf(stderr, "dma: width must be a multiple of %u px\n", kWaves * 512u);
+        exit(2);
+    }
+    (void)dma::dma_go<kVarFastDiv, kWaves>(static_cast<const uint8_t*>(in), static_cast<float*>(out), c.g, c.qp, c.cus,
+                                           kWgsPerCu, s);
+}
+
+// banded persistent schedule with register prefetch (kbench_band.hpp)
+template <typename TOut, unsigned kVar, uint32_t kWavesPerCU>
+void band_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    (void)band::band_go<TOut, kVar>(static_cast<const uint8_t*>(in), static_cast<TOut*>(out), c.g, c.qp, c.cus,
+                                    kWavesPerCU, s);
+}
+template <unsigned kVar>
+void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+// ---- access-pattern probes (no arithmetic; values are not a transform) ----
+// The headline kernel's traffic per 64-tile set (8 row loads of 512 B, 16 NT
+// stores of 1 KiB) issued by W persistent waves that walk the sets in bands
+// (set = j * W + wave: at step j all waves work on consecutive sets, so the
+// chip-wide write front is W x 16 KiB) with the next set's rows prefetched
+// into registers; W = kWavesPerCU x CUs.
+template <bool kPrefetch>
+__global__ __launch_bounds__(256) void pat_band(const uint8_t* __restrict__ in, float* __restrict__ out, TileGrid g,
+                                                uint32_t nsets) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * 4u;
+    uint32_t s = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    auto base_of = [&](uint32_t set) {
+        const uint32_t t0 = set * 64u, ty = t0 / g.tiles_x, tx = t0 - ty * g.tiles_x;
+        return static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(tx) * 8u;
+    };
+    uint2 r[8];
+    if (s >= nsets) return;
+    unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(in + base_of(s) + i * g.width + 8u * lane); });
+    for (; s < nsets; s += nw) {
+        uint2 nx[8];
+        const bool more = kPrefetch && s + nw < nsets;
+        if (more) {
+            unroll<8>([&](auto i) { nx[i] = *reinterpret_cast<const uint2*>(in + base_of(s + nw) + i * g.width + 8u * lane); });
+        }
+        float* o = out + base_of(s);
+        unroll<8>([&](auto i) {
+            const float4 a = make_float4((float)(r[i].x & 255u), (float)(r[i].x >> 24), (float)(r[i].y & 255u),
+                                         (float)(r[i].y >> 24));
+            st_at<true>(o + i * g.width, 16u * lane, a);
+            st_at<true>(o + i * g.width, 1024u + 16u * lane, a);
+        });
+        if constexpr (kPrefetch) {
+            if (more) unroll<8>([&](auto i) { r[i] = nx[i]; });
+        } else if (s + nw < nsets) {
+            unroll<8>([&](auto i) { r[i] = *reinterpret_cast<const uint2*>(in + base_of(s + nw) + i * g.width + 8u * lane); });
+        }
+    }
+}
+template <uint32_t kWavesPerCU, bool kPrefetch>
+void pat_band_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t nsets = c.g.ntiles / 64u;
+    hipLaunchKernelGGL((pat_band<kPrefetch>), dim3(std::min(nsets / 4u, c.cus * kWavesPerCU / 4u)), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), c.g, nsets);
+}
+// the same traffic, one set per wave, non-persistent (the product's dispatch)
+void pat_grid_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t nsets = c.g.ntiles / 64u;
+    hipLaunchKernelGGL((pat_band<false>), dim3(nsets / 4u), dim3(256), 0, s, static_cast<const uint8_t*>(in),
+                       static_cast<float*>(out), c.g, nsets);
+}
+
+int main(int argc, char** argv) {
+    int n = 8192, hgt = 8192;
+    if (argc > 1) {
+        n = hgt = atoi(argv[1]);
+        if (const char* x = strchr(argv[1], 'x')) n = atoi(x + 1);
+    }
+    const int iters = argc > 2 ? atoi(argv[2]) : 64;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+    const std::string only = argc > 4 ? argv[4] : "all";
+    const int nsets = argc > 5 ? atoi(argv[5]) : 16;
+    const size_t px = (size_t)hgt * n;
+    Ctx c;
+    c.g = TileGrid{(uint32_t)(px / 64), (uint32_t)(n / 8), (uint64_t)n};
+    for (int i = 0; i < 64; ++i) {
+        c.qp.q.v[i] = kDefaultQ.v[i];
+        c.qp.r.v[i] = 1.0f / kDefaultQ.v[i];
+    }
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    c.cus = (uint32_t)cus;
+
+    constexpr unsigned F = kVarFastDiv;
+    constexpr unsigned P = kProdVar<uint8_t, float> | F;
+    constexpr unsigned I8 = kProdVar<uint8_t, int8_t> | F;
+    std::vector<Variant> vars = {
+        {"fwd", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 8w x 2/cu", dma_f32_fwd<8, 2>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 8w x 1/cu", dma_f32_fwd<8, 1>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 4w x 4/cu", dma_f32_fwd<4, 4>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 4w x 2/cu", dma_f32_fwd<4, 2>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 8w not persistent", dma_f32_fwd<8, 64>, 5, 4, true},
+        {"fwd", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"fwd", "fwd u8->f32 dma 8w x 2/cu again", dma_f32_fwd<8, 2>, 5, 4, true},
+        {"band", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"band", "fwd u8->f32 band 4 w/cu", band_fwd<float, (P & ~(3u << 12)), 4>, 5, 4, true},
+        {"band", "fwd u8->f32 band 8 w/cu b256", band_fwd<float, (P & ~(3u << 12)), 8>, 5, 4, true},
+        {"band", "fwd u8->f32 band 8 w/cu b512", band_fwd<float, P, 8>, 5, 4, true},
+        {"band", "fwd u8->f32 band 16 w/cu b512", band_fwd<float, P, 16>, 5, 4, true},
+        {"band", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"band", "fwd u8->f32 band 4 w/cu again", band_fwd<float, (P & ~(3u << 12)), 4>, 5, 4, true},
+        {"bandi8", "fwd u8->i8 library (b512)", prod_i8_fwd<I8>, 2, 1, true},
+        {"bandi8", "fwd u8->i8 band 4 w/cu", band_fwd<int8_t, (I8 & ~(3u << 12)), 4>, 2, 1, true},
+        {"bandi8", "fwd u8->i8 band 8 w/cu b256", band_fwd<int8_t, (I8 & ~(3u << 12)), 8>, 2, 1, true},
+        {"bandi8", "fwd u8->i8 band 16 w/cu b512", band_fwd<int8_t, I8, 16>, 2, 1, true},
+        {"bandi8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
+        {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
+        {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},
+        {"pat", "pat band 8 w/cu", pat_band_go<8, false>, 5, 4, false},
+        {"pat", "pat band 8 w/cu prefetch", pat_band_go<8, true>, 5, 4, false},
+        {"pat", "pat band 16 w/cu", pat_band_go<16, false>, 5, 4, false},
+        {"pat", "pat band 16 w/cu prefetch", pat_band_go<16, true>, 5, 4, false},
+        {"pat", "pat band 32 w/cu", pat_band_go<32, false>, 5, 4, false},
+        {"pat", "pat one set per wave (grid) again", pat_grid_go, 5, 4, false},
+        {"pat", "pat band 2 w/cu prefetch", pat_band_go<2, true>, 5, 4, false},
+    };
+    vars.erase(std::remove_if(vars.begin(), vars.end(),
+                              [&](const Variant& v) { return only != "all" && v.group != only; }),
+               vars.end());
+
+    std::vector<uint8_t*> img(nsets);
+    std::vector<void*> out(nsets);
+    std::vector<uint8_t> h(px);
+    srand(42);
+    for (size_t i = 0; i < px; ++i) h[i] = (uint8_t)(rand() % 256);
+    for (int s = 0; s < nsets; ++s) {
+        CK(hipMalloc(&img[s], px));
+        CK(hipMalloc(&out[s], px * 4));
+        if (s == 0) {
+            CK(hipMemcpy(img[s], h.data(), px, hipMemcpyHostToDevice));
+        } else {
+            CK(launch_fill_hash_impl(img[s], px, 1000u + s, 0, 0));
+        }
+    }
+    CK(hipDeviceSynchronize());
+    // correctness: each variant against its group's first entry, on sets 0 and 1
+    {
+        std::vector<uint8_t> ref(px * 4), got(px * 4);
+        for (int s = 0; s < 2; ++s) {
+            std::string cur;
+            for (auto& v : vars) {
+                const size_t nb = px * v.obpp;
+                CK(hipMemset(out[2], 0xa5, nb));
+                v.launch(img[s], out[2], c, 0);
+                const hipError_t le = hipGetLastError();
+                if (le != hipSuccess) {
+                    printf("check %-40s LAUNCH FAILED: %s\n", v.name.c_str(), hipGetErrorString(le));
+                    return 1;
+                }
+                CK(hipDeviceSynchronize());
+                if (v.group != cur) {
+                    cur = v.group;
+                    CK(hipMemcpy(ref.data(), out[2], nb, hipMemcpyDeviceToHost));
+                    continue;
+                }
+                if (!v.check) continue;
+                CK(hipMemcpy(got.data(), out[2], nb, hipMemcpyDeviceToHost));
+                size_t bad = 0;
+                for (size_t i = 0; i < nb; ++i) bad += ref[i] != got[i];
+                printf("check set %d %-40s %s", s, v.name.c_str(), bad ? "MISMATCH" : "bit-exact\n");
+                if (bad) {
+                    printf(" (%zu bytes)\n", bad);
+                    return 1;
+                }
+            }
+        }
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<std::vector<float>> us(vars.size());
+    for (int r = 0; r < rounds; ++r) {
+        for (size_t v = 0; v < vars.size(); ++v) {
+            for (int w = 0; w < 2 * nsets; ++w) vars[v].launch(img[w % nsets], out[w % nsets], c, 0);
+            for (int i = 0; i < iters; i += nsets) {
+                CK(hipEventRecord(a, 0));
+                for (int k = 0; k < nsets; ++k) vars[v].launch(img[k], out[k], c, 0);
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, a, b));
+                us[v].push_back(ms * 1e3f / nsets);
+            }
+        }
+    }
+    printf("%-42s %10s %10s %6s %8s\n", "variant", "median_us", "min_us", "B/px", "frac8T");
+    for (size_t v = 0; v < vars.size(); ++v) {
+        auto t = us[v];
+        std::sort(t.begin(), t.end());
+        const double med = t[t.size() / 2];
+        printf("%-42s %10.2f %10.2f %6.0f %8.3f\n", vars[v].name.c_str(), med, t[0], vars[v].bpp,
+               vars[v].bpp * px / (med * 1e-6) / 8e12);
+    }
+    return 0;
+}
