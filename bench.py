@@ -45,7 +45,8 @@ sys.path.insert(0, os.path.join(ROOT, "cuda-dct-idct_amd"))
 METRIC = "Gpixel/s fwd-DCT (8192×8192) + achieved HBM % at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 T4_FWD_8192_MS = 14.70         # README.md:55, T4
-BYTES_PER_PX = {"u8_f32": 5, "f32_f32": 8, "u8_i8": 2, "inv_f32_f32": 8}
+BYTES_PER_PX = {"u8_f32": 5, "f32_f32": 8, "u8_i8": 2, "inv_f32_f32": 8,
+                "compat_fwd": 12, "compat_inv": 8, "compat_inv_wb": 12}
 EXTRA_STEPS = 100              # timed launches per extra (independent of --steps)
 EXTRA_WARM_S = 0.02            # untimed steady-state lead-in per extra (>= 20 ms)
 MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MI355X_MICROARCH.md)
@@ -366,6 +367,44 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         rms, k, _ = timed_loop(calls, steps, 5)
         extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world,
                                       "idct_f32_f32_duo", n)
+        # the drop-in surface: exactly what the compat entry points launch
+        # (hpdct_compat.cpp), i.e. what a caller of the reference's functions
+        # gets: fp32 planes, the caller's T, and the reference's in-place side
+        # effects (X-128 left in the image, main_newAppr.cu:273; q*Q left in the
+        # coefficients by the cublasDCTv2 inverse, main_cublass_2.cu:285).  The
+        # write-backs change the inputs from launch to launch; the kernels' time
+        # does not depend on the values.
+        dropin = {}
+        calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, writeback_shift=True, stream=stream)
+                 for i in range(len(f32_in))]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        dropin["dct_all_blocks_cuda"] = dict(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_f32_wb", n),
+            launches="fdct_duo_kernel<quant, runtime T, writeback>",
+            bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
+        calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, stream=stream) for s in range(args.sets)]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        dropin["idct_all_blocks_cuda"] = dict(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv"], world, "compat_inv_f32", n),
+            launches="idct_duo_kernel<dequant, runtime T>", bytes_note="4 B read + 4 B written")
+        calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, writeback_shift=True, row_first=True,
+                            stream=stream) for i in range(len(f32_in))]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        dropin["dct_all_blocks (cublasDCTv2)"] = dict(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_rowfirst_wb", n),
+            launches="rowfirst_duo_kernel<forward, quant, runtime T, writeback>",
+            bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
+        calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, row_first=True, writeback_dequant=True,
+                            stream=stream) for s in range(args.sets)]
+        rms, k, _ = timed_loop(calls, steps, 5)
+        dropin["idct_all_blocks (cublasDCTv2)"] = dict(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv_wb"], world, "compat_inv_rowfirst_wb",
+                  n),
+            launches="rowfirst_duo_kernel<inverse, dequant, runtime T, writeback>",
+            bytes_note="4 B read + 4 B pixels + 4 B q*Q written back")
+        extras["dropin"] = dropin
+        # the write-backs above changed the fp32 inputs / coefficients: the
+        # later extras recompute what they read
         # the reference's own two GPU decompositions of the same arithmetic, on
         # this GPU (include/hpdct_baseline.h): 3 launches per frame, fp32 in/out
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
@@ -428,7 +467,9 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                                   "kernel; bit-identical to the two kernels"),
             "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
                                        note="hpdct_roundtrip_u8_accumulate into a caller-zeroed ring of 1024 "
-                                            "per-frame sums slots (one memset per ring, not per launch)"),
+                                            "per-frame sums slots; the ring's one memset per 1024 frames is "
+                                            "outside the timed region (amortised: ~3 ns per frame), and slots "
+                                            "reused by the warm-up accumulate (the timing does not depend on it)"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
         del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it

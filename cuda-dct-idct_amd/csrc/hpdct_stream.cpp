@@ -10,107 +10,194 @@
 // operations are ordered, which makes its buffer reuse safe.  Host buffers
 // should be pinned (hipHostMalloc / torch pin_memory) for the copies to be
 // asynchronous and overlap.
+//
+// The streams, device ring and timing events live in an hpdct_stream_ctx
+// (hpdct_stream_create / _run / _destroy), so a caller that streams many
+// batches pays their creation once; hpdct_stream_forward is the one-shot
+// form (create, run, destroy).
 #include <hip/hip_runtime.h>
 
+#include <new>
 #include <string>
 #include <vector>
 
 #include "hpdct.h"
 #include "hpdct_kernels.h"
 
+struct hpdct_stream_ctx_s {
+    int64_t height = 0, width = 0;
+    hpdct_dtype out_type = HPDCT_F32;
+    int device = -1;
+    std::vector<hipStream_t> streams;
+    std::vector<void*> in, out;
+    std::vector<hipEvent_t> done;  // per stream: its last operation of a batch
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+
+    ~hpdct_stream_ctx_s() {
+        for (void* p : in) (void)hipFree(p);
+        for (void* p : out) (void)hipFree(p);
+        for (hipEvent_t e : done) (void)hipEventDestroy(e);
+        if (t0) (void)hipEventDestroy(t0);
+        if (t1) (void)hipEventDestroy(t1);
+        for (hipStream_t s : streams) (void)hipStreamDestroy(s);
+    }
+};
+
 namespace {
 hpdct_status fail(hpdct_status st, const std::string& msg) {
     return static_cast<hpdct_status>(hpdct::set_last_error(st, msg.c_str()));
 }
 hpdct_status device_fail(hipError_t e, const char* what) {
-    return fail(HPDCT_ERROR_DEVICE, std::string("hpdct_stream_forward: ") + what + ": " + hipGetErrorString(e));
+    return fail(HPDCT_ERROR_DEVICE, std::string("hpdct stream: ") + what + ": " + hipGetErrorString(e));
 }
 
-struct DeviceRing {
-    std::vector<hipStream_t> streams;
-    std::vector<void*> in, out;
-    ~DeviceRing() {
-        for (void* p : in) (void)hipFree(p);
-        for (void* p : out) (void)hipFree(p);
-        for (hipStream_t s : streams) (void)hipStreamDestroy(s);
-    }
-};
-}  // namespace
-
-extern "C" hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
-                                             int64_t height, int64_t width, hpdct_dtype out_type, int nstreams,
-                                             float* elapsed_ms) {
-    if (!h_frames || !h_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: null frame list");
-    if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: negative frame count");
+hpdct_status validate(int64_t height, int64_t width, hpdct_dtype out_type, int nstreams) {
     if (nstreams < 1 || nstreams > 16)
-        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: nstreams must be in 1..16");
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct stream: nstreams must be in 1..16");
     if (out_type != HPDCT_F32 && out_type != HPDCT_I8)
-        return fail(HPDCT_ERROR_UNSUPPORTED, "hpdct_stream_forward: output must be HPDCT_F32 or HPDCT_I8");
+        return fail(HPDCT_ERROR_UNSUPPORTED, "hpdct stream: output must be HPDCT_F32 or HPDCT_I8");
     if (height <= 0 || width <= 0 || height % 8 || width % 8)
-        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: height and width must be positive multiples of 8");
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct stream: height and width must be positive multiples of 8");
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status create(hpdct_stream_ctx* out_ctx, int64_t height, int64_t width, hpdct_dtype out_type, int nstreams) {
+    if (!out_ctx) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_create: null handle pointer");
+    *out_ctx = nullptr;
+    if (hpdct_status st = validate(height, width, out_type, nstreams)) return st;
+    hpdct_stream_ctx c = new (std::nothrow) hpdct_stream_ctx_s;
+    if (!c) return fail(HPDCT_ERROR_DEVICE, "hpdct stream: out of host memory");
+    c->height = height;
+    c->width = width;
+    c->out_type = out_type;
+    const size_t px = static_cast<size_t>(height) * static_cast<size_t>(width);
+    const size_t out_bytes = px * (out_type == HPDCT_F32 ? 4 : 1);
+    hipError_t he = hipGetDevice(&c->device);
+    for (int s = 0; s < nstreams && he == hipSuccess; ++s) {
+        hipStream_t st;
+        void *di = nullptr, *dout = nullptr;
+        hipEvent_t ev;
+        if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) break;
+        c->streams.push_back(st);
+        if ((he = hipMalloc(&di, px)) != hipSuccess) break;
+        c->in.push_back(di);
+        if ((he = hipMalloc(&dout, out_bytes)) != hipSuccess) break;
+        c->out.push_back(dout);
+        if ((he = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
+        c->done.push_back(ev);
+    }
+    if (he == hipSuccess) he = hipEventCreate(&c->t0);
+    if (he == hipSuccess) he = hipEventCreate(&c->t1);
+    if (he != hipSuccess) {
+        delete c;
+        return device_fail(he, "creating the streams / device ring");
+    }
+    *out_ctx = c;
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status run(hpdct_stream_ctx c, const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
+                 float* elapsed_ms) {
+    if (!c) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_run: null context");
+    if (!h_frames || !h_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct stream: null frame list");
+    if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct stream: negative frame count");
     for (int64_t f = 0; f < n_frames; ++f)
         if (!h_frames[f] || !h_coef[f])
-            return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: null frame or output pointer at index " +
-                                                       std::to_string(f));
+            return fail(HPDCT_ERROR_INVALID_VALUE,
+                        "hpdct stream: null frame or output pointer at index " + std::to_string(f));
     if (n_frames == 0) {
         if (elapsed_ms) *elapsed_ms = 0.0f;
         return HPDCT_SUCCESS;
     }
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
+        return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_run: the context belongs to device " +
+                                                   std::to_string(c->device) + ", the current device is " +
+                                                   std::to_string(cur));
+    const int64_t height = c->height, width = c->width;
     const size_t px = static_cast<size_t>(height) * static_cast<size_t>(width);
-    const size_t out_bytes = px * (out_type == HPDCT_F32 ? 4 : 1);
-    DeviceRing ring;
-    for (int s = 0; s < nstreams; ++s) {
-        hipStream_t st;
-        void *di = nullptr, *dout = nullptr;
-        hipError_t he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-        if (he != hipSuccess) return device_fail(he, "hipStreamCreateWithFlags");
-        ring.streams.push_back(st);
-        if ((he = hipMalloc(&di, px)) != hipSuccess) return device_fail(he, "hipMalloc (frames)");
-        ring.in.push_back(di);
-        if ((he = hipMalloc(&dout, out_bytes)) != hipSuccess) return device_fail(he, "hipMalloc (coefficients)");
-        ring.out.push_back(dout);
-    }
-    hipEvent_t t0, t1;
-    if (hipError_t he = hipEventCreate(&t0); he != hipSuccess) return device_fail(he, "hipEventCreate");
-    if (hipError_t he = hipEventCreate(&t1); he != hipSuccess) {
-        (void)hipEventDestroy(t0);
-        return device_fail(he, "hipEventCreate");
-    }
+    const size_t out_bytes = px * (c->out_type == HPDCT_F32 ? 4 : 1);
+    const int nstreams = static_cast<int>(c->streams.size());
     // start marker: every stream waits for it, so the timed region holds the whole batch
-    hipError_t e = hipEventRecord(t0, ring.streams[0]);
-    for (int s = 1; s < nstreams && e == hipSuccess; ++s) e = hipStreamWaitEvent(ring.streams[s], t0, 0);
+    hipError_t e = hipEventRecord(c->t0, c->streams[0]);
+    for (int s = 1; s < nstreams && e == hipSuccess; ++s) e = hipStreamWaitEvent(c->streams[s], c->t0, 0);
     for (int64_t f = 0; f < n_frames && e == hipSuccess; ++f) {
         const int s = static_cast<int>(f % nstreams);
-        hipStream_t st = ring.streams[s];
-        e = hipMemcpyAsync(ring.in[s], h_frames[f], px, hipMemcpyHostToDevice, st);
+        hipStream_t st = c->streams[s];
+        e = hipMemcpyAsync(c->in[s], h_frames[f], px, hipMemcpyHostToDevice, st);
         if (e != hipSuccess) break;
-        const hpdct_status hs = hpdct_forward(ring.in[s], HPDCT_U8, ring.out[s], out_type, height, width, nullptr,
-                                              0u, st);
+        const hpdct_status hs =
+            hpdct_forward(c->in[s], HPDCT_U8, c->out[s], c->out_type, height, width, nullptr, 0u, st);
         if (hs != HPDCT_SUCCESS) {
-            (void)hipEventDestroy(t0);
-            (void)hipEventDestroy(t1);
-            (void)hipDeviceSynchronize();
+            for (hipStream_t x : c->streams) (void)hipStreamSynchronize(x);
             return hs;
         }
-        e = hipMemcpyAsync(h_coef[f], ring.out[s], out_bytes, hipMemcpyDeviceToHost, st);
+        e = hipMemcpyAsync(h_coef[f], c->out[s], out_bytes, hipMemcpyDeviceToHost, st);
     }
     // end marker after every stream's last operation
     for (int s = 1; s < nstreams && e == hipSuccess; ++s) {
-        hipEvent_t done;
-        e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
-        if (e != hipSuccess) break;
-        e = hipEventRecord(done, ring.streams[s]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ring.streams[0], done, 0);
-        (void)hipEventDestroy(done);
+        e = hipEventRecord(c->done[s], c->streams[s]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->streams[0], c->done[s], 0);
     }
-    if (e == hipSuccess) e = hipEventRecord(t1, ring.streams[0]);
-    if (e == hipSuccess) e = hipEventSynchronize(t1);
+    if (e == hipSuccess) e = hipEventRecord(c->t1, c->streams[0]);
+    if (e == hipSuccess) e = hipEventSynchronize(c->t1);
     float ms = 0.0f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
-    for (hipStream_t st : ring.streams) (void)hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->t0, c->t1);
+    for (hipStream_t st : c->streams) (void)hipStreamSynchronize(st);
     if (e != hipSuccess) return device_fail(e, "copy/compute pipeline");
     if (elapsed_ms) *elapsed_ms = ms;
     return HPDCT_SUCCESS;
 }
+
+// no C++ exception may cross the C ABI
+template <typename F>
+hpdct_status guarded(const char* what, F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& ex) {
+        return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": " + ex.what());
+    } catch (...) {
+        return fail(HPDCT_ERROR_DEVICE, std::string(what) + ": host exception");
+    }
+}
+}  // namespace
+
+extern "C" {
+
+hpdct_status hpdct_stream_create(hpdct_stream_ctx* ctx, int64_t height, int64_t width, hpdct_dtype out_type,
+                                 int nstreams) {
+    return guarded("hpdct_stream_create", [&] { return create(ctx, height, width, out_type, nstreams); });
+}
+
+hpdct_status hpdct_stream_run(hpdct_stream_ctx ctx, const uint8_t* const* h_frames, void* const* h_coef,
+                              int64_t n_frames, float* elapsed_ms) {
+    return guarded("hpdct_stream_run", [&] { return run(ctx, h_frames, h_coef, n_frames, elapsed_ms); });
+}
+
+hpdct_status hpdct_stream_destroy(hpdct_stream_ctx ctx) {
+    delete ctx;  // run() leaves every stream idle, so the ring is free to go
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
+                                  int64_t height, int64_t width, hpdct_dtype out_type, int nstreams,
+                                  float* elapsed_ms) {
+    if (!h_frames || !h_coef) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: null frame list");
+    if (n_frames < 0) return fail(HPDCT_ERROR_INVALID_VALUE, "hpdct_stream_forward: negative frame count");
+    if (hpdct_status st = validate(height, width, out_type, nstreams)) return st;
+    for (int64_t f = 0; f < n_frames; ++f)
+        if (!h_frames[f] || !h_coef[f])
+            return fail(HPDCT_ERROR_INVALID_VALUE,
+                        "hpdct_stream_forward: null frame or output pointer at index " + std::to_string(f));
+    if (n_frames == 0) {  // nothing to stream: no device resources either
+        if (elapsed_ms) *elapsed_ms = 0.0f;
+        return HPDCT_SUCCESS;
+    }
+    hpdct_stream_ctx c = nullptr;
+    if (hpdct_status st = hpdct_stream_create(&c, height, width, out_type, nstreams)) return st;
+    const hpdct_status st = hpdct_stream_run(c, h_frames, h_coef, n_frames, elapsed_ms);
+    hpdct_stream_destroy(c);
+    return st;
+}
+
+}  // extern "C"

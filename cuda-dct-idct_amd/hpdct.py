@@ -50,6 +50,7 @@ C_SYMBOLS = [
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
     "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate", "hpdct_forward_frames",
+    "hpdct_stream_create", "hpdct_stream_run", "hpdct_stream_destroy",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -127,6 +128,11 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_get_mapping.restype = ctypes.c_int
     lib.hpdct_stream_forward.argtypes = [vp, vp, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp]
     lib.hpdct_stream_forward.restype = ctypes.c_int
+    lib.hpdct_stream_create.argtypes = [vp, i64, i64, ctypes.c_int, ctypes.c_int]
+    lib.hpdct_stream_run.argtypes = [vp, vp, vp, i64, vp]
+    lib.hpdct_stream_destroy.argtypes = [vp]
+    for f in (lib.hpdct_stream_create, lib.hpdct_stream_run, lib.hpdct_stream_destroy):
+        f.restype = ctypes.c_int
     lib.hpdct_forward_frames.argtypes = [vp, vp, ctypes.c_int, i64, i64, i64, vp]
     lib.hpdct_forward_frames.restype = ctypes.c_int
     lib.hpdct_baseline_forward.argtypes = [ctypes.c_int, vp, vp, vp, i64, i64, vp, vp]
@@ -314,7 +320,7 @@ def inverse(coef, out=None, *, out_dtype=None, transform=None, dequantise=True, 
 
 
 def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift=True, writeback_shift=False,
-         stream=None, height=None, width=None):
+         row_first=False, writeback_dequant=False, stream=None, height=None, width=None):
     """Pre-resolve every argument of one forward ("fwd") or inverse ("inv")
     launch and return a zero-argument callable: the per-call host cost is one
     ctypes call (used by bench.py's timed loop)."""
@@ -324,7 +330,8 @@ def bind(direction: str, src, dst, *, transform=None, quantise=True, level_shift
     lib = load_library()
     fn = {"fwd": lib.hpdct_forward, "inv": lib.hpdct_inverse}[direction]
     flags = (0 if quantise else FLAG_NO_QUANT) | (0 if level_shift else FLAG_NO_SHIFT) | \
-        (FLAG_WRITEBACK_SHIFT if writeback_shift else 0)
+        (FLAG_WRITEBACK_SHIFT if writeback_shift else 0) | (FLAG_ROW_FIRST if row_first else 0) | \
+        (FLAG_WRITEBACK_DEQUANT if writeback_dequant else 0)
     args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(dst.data_ptr()), _dtype_code(dst),
             h, w, _transform_ptr(transform, src.device), flags, _stream_ptr(stream))
 
@@ -488,11 +495,8 @@ def bind_frames(frames, outs, *, stream=None):
     return call
 
 
-def stream_forward(frames, outs, nstreams: int = 3) -> float:
-    """Config C5: host-resident (pinned) uint8 frames -> host coefficient planes
-    with H2D / kernel / D2H overlapped over `nstreams` HIP streams.  `frames`
-    and `outs` are equal-length lists of CPU tensors (entries may repeat).
-    Returns the device-timed milliseconds of the whole batch."""
+def _stream_lists(frames, outs):
+    """Checks of a C5 batch; returns (n, h, w, out dtype code, frame and out pointer arrays)."""
     torch = _torch()
     n = len(frames)
     if n != len(outs) or n == 0:
@@ -514,10 +518,64 @@ def stream_forward(frames, outs, nstreams: int = 3) -> float:
             raise HpdctError(1, f"out {i}: expected {h * w} {odt} elements, got {o.numel()} {o.dtype}")
     fp = (ctypes.c_void_p * n)(*[f.data_ptr() for f in frames])
     op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    return n, h, w, _dtype_code(outs[0]), fp, op
+
+
+def stream_forward(frames, outs, nstreams: int = 3) -> float:
+    """Config C5: host-resident (pinned) uint8 frames -> host coefficient planes
+    with H2D / kernel / D2H overlapped over `nstreams` HIP streams.  `frames`
+    and `outs` are equal-length lists of CPU tensors (entries may repeat).
+    Returns the device-timed milliseconds of the whole batch.  One-shot:
+    streams and device buffers are made and freed per call (StreamContext
+    keeps them)."""
+    n, h, w, odt, fp, op = _stream_lists(frames, outs)
     ms = ctypes.c_float()
-    _check(load_library().hpdct_stream_forward(fp, op, n, h, w, _dtype_code(outs[0]), int(nstreams),
-                                               ctypes.byref(ms)))
+    _check(load_library().hpdct_stream_forward(fp, op, n, h, w, odt, int(nstreams), ctypes.byref(ms)))
     return ms.value
+
+
+class StreamContext:
+    """A persistent C5 pipeline (hpdct_stream_create / _run / _destroy): the
+    HIP streams, the device ring (one input + one output frame per stream)
+    and the timing events are created once, on the current device, for
+    height x width frames and one coefficient dtype; run() streams a batch
+    through them like stream_forward()."""
+
+    def __init__(self, height: int, width: int, out_dtype, nstreams: int = 3):
+        torch = _torch()
+        if out_dtype not in (torch.float32, torch.int8):
+            raise HpdctError(2, f"coefficient planes must be float32 or int8, not {out_dtype}")
+        self.height, self.width, self.out_dtype = int(height), int(width), out_dtype
+        self.handle = ctypes.c_void_p()
+        _check(load_library().hpdct_stream_create(ctypes.byref(self.handle), self.height, self.width,
+                                                  F32 if out_dtype == torch.float32 else I8, int(nstreams)))
+
+    def run(self, frames, outs) -> float:
+        if not self.handle:
+            raise HpdctError(1, "stream context is closed")
+        n, h, w, _, fp, op = _stream_lists(frames, outs)
+        if (h, w) != (self.height, self.width) or outs[0].dtype != self.out_dtype:
+            raise HpdctError(1, f"context is for {self.height}x{self.width} -> {self.out_dtype} frames")
+        ms = ctypes.c_float()
+        _check(load_library().hpdct_stream_run(self.handle, fp, op, n, ctypes.byref(ms)))
+        return ms.value
+
+    def close(self) -> None:
+        if self.handle:
+            _check(load_library().hpdct_stream_destroy(self.handle))
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):

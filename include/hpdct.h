@@ -193,6 +193,20 @@ hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h
                                   int64_t height, int64_t width, hpdct_dtype out_type, int nstreams,
                                   float* elapsed_ms);
 
+/* The same pipeline with its resources kept across calls: hpdct_stream_create
+ * makes the nstreams HIP streams, their device input/output buffers (one
+ * height x width frame each) and the timing events on the current device;
+ * hpdct_stream_run streams one batch through them (semantics and timing as
+ * hpdct_stream_forward, on the context's device); hpdct_stream_destroy frees
+ * them.  hpdct_stream_forward is create + run + destroy.  A context is not
+ * thread-safe: one run at a time. */
+typedef struct hpdct_stream_ctx_s* hpdct_stream_ctx;
+hpdct_status hpdct_stream_create(hpdct_stream_ctx* ctx, int64_t height, int64_t width, hpdct_dtype out_type,
+                                 int nstreams);
+hpdct_status hpdct_stream_run(hpdct_stream_ctx ctx, const uint8_t* const* h_frames, void* const* h_coef,
+                              int64_t n_frames, float* elapsed_ms);
+hpdct_status hpdct_stream_destroy(hpdct_stream_ctx ctx);
+
 /* Synthetic frames generated on the device (BASELINE config C4): pixel
  * i of the frame = splitmix64(seed, first_index + i) & 255 (the oracle's
  * oracle_fill_hash_u8 restates it). */

@@ -169,3 +169,23 @@ def test_forward_frames_checks_every_plane(hp, t):
     with pytest.raises(hp.HpdctError):
         hp.forward_frames([FakeDev((64, 64), t.uint8, contiguous=False)], [o])
     assert hp.forward_frames([], []) == []
+
+
+def test_stream_context_arguments_rejected(hp):
+    """hpdct_stream_create validates before touching a device; run/destroy
+    on a NULL context are a status / a no-op."""
+    import ctypes
+    L = hp.load_library()
+    h = ctypes.c_void_p()
+    assert L.hpdct_stream_create(ctypes.byref(h), 64, 64, hp.F32, 0) == 1    # nstreams 0
+    assert L.hpdct_stream_create(ctypes.byref(h), 64, 64, hp.F32, 17) == 1   # > 16
+    assert L.hpdct_stream_create(ctypes.byref(h), 64, 64, hp.U8, 2) == 2     # coefficients f32 / i8
+    assert L.hpdct_stream_create(ctypes.byref(h), 64, 60, hp.F32, 2) == 1    # width not a multiple of 8
+    assert L.hpdct_stream_create(None, 64, 64, hp.F32, 2) == 1
+    assert not h.value
+    P = ctypes.c_void_p * 1
+    assert L.hpdct_stream_run(None, P(1), P(1), 1, None) == 1
+    assert L.hpdct_stream_destroy(None) == 0
+    # the one-shot form: an empty batch is a no-op without device work
+    ms = ctypes.c_float(-1.0)
+    assert L.hpdct_stream_forward(P(1), P(1), 0, 64, 64, hp.F32, 2, ctypes.byref(ms)) == 0 and ms.value == 0.0
