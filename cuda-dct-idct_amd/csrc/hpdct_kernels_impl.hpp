@@ -39,9 +39,6 @@ enum : unsigned {
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
-    kVarRowsFirst = 1u << 21, // forward: the first pass issued input row by input row (fdct_tile_rows_first)
-    kVarFusedQ = 1u << 26,    // quantiser as trunc(fma(C, r, copysign(0.49999997, C))), r = RN(1/Q): 3 operations
-                              // instead of 6; exact only for the divisors tests/tools/verify_quant1.hip proves
     kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
                               // multiple of 512 px) stores two contiguous runs per instruction instead of
                               // 32 B per lane; launched only for such widths (the branch costs the
@@ -160,10 +157,6 @@ __device__ __forceinline__ void cvt_into_byte(uint32_t& w, float biased) {
 // divide_matrices (utils_kernels.cu:42): round(C / Q)
 template <unsigned kVar>
 __device__ __forceinline__ float quantise(float c, float q, float r) {
-    if constexpr (kVar & kVarFusedQ) {
-        (void)q;
-        return __builtin_truncf(__builtin_fmaf(c, r, signed_half(c)));
-    }
     float d;
     if constexpr (kVar & kVarFastDiv) {
         const float q0 = c * r;
@@ -207,13 +200,6 @@ struct RawTile<uint8_t> {  // 8 rows x 8 bytes = 16 VGPRs
                 x[i][j] = byte_f32(r[i].x, j) - shift;
                 x[i][j + 4] = byte_f32(r[i].y, j) - shift;
             });
-        });
-    }
-    // row i alone (fdct_tile_rows_first), as to_float
-    __device__ __forceinline__ void row(int i, float (&xr)[8], float shift) const {
-        unroll<4>([&](auto j) {
-            xr[j] = byte_f32(r[i].x, j) - shift;
-            xr[j + 4] = byte_f32(r[i].y, j) - shift;
         });
     }
     // X - 128 exactly: (int8_t)(b ^ 0x80) == b - 128 for b in 0..255 (the round
@@ -473,23 +459,13 @@ __device__ __forceinline__ void fdct_body(const TIn* __restrict__ img, TOut* __r
 
     walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         float x[8][8];
-        if constexpr ((kVar & kVarRowsFirst) == 0 || !std::is_same_v<TIn, uint8_t>) raw.to_float(x, shift);
+        raw.to_float(x, shift);
         if constexpr (kWriteback) {
             // the reference leaves X-128 in its input (main_newAppr.cu:273)
             unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
         }
         auto emit = [&](auto v, float (&c)[8]) {
-            if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0 &&
-                          (kVar & kVarFusedQ) != 0) {
-                // the biased quotient in one fma; the truncating convert finishes the rounding
-                uint32_t w0 = 0u, w1 = 0u;
-                unroll<4>([&](auto u) {
-                    cvt_into_byte<u>(w0, __builtin_fmaf(c[u], qp.r.v[v * 8 + u], signed_half(c[u])));
-                    cvt_into_byte<u>(w1, __builtin_fmaf(c[u + 4], qp.r.v[v * 8 + u + 4], signed_half(c[u + 4])));
-                });
-                st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), make_uint2(w0, w1));
-                return;
-            } else if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
+            if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
                 unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
                 const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
                 st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
@@ -502,10 +478,6 @@ __device__ __forceinline__ void fdct_body(const TIn* __restrict__ img, TOut* __r
         };
         if constexpr ((kVar & kVarRowFirst) != 0) {
             fdct_tile_rowfirst(T, x, emit);
-        } else if constexpr ((kVar & kVarRowsFirst) != 0 && std::is_same_v<TIn, uint8_t>) {
-            (void)x;
-            fdct_tile_rows_first(
-                T, [&](auto i, float (&xr)[8]) { raw.row(i, xr, shift); }, emit);
         } else {
             fdct_tile(T, x, emit);
         }

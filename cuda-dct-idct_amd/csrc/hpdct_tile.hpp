@@ -117,38 +117,6 @@ __device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& 
     });
 }
 
-// The same forward with the first pass issued row by row: every chain
-// P[v][col] still runs over i = 0..7 in order from +0 (bit-identical), but
-// input row i is converted (row_of(i, xr)) and all the FMAs that consume it
-// are issued before row i+1 is touched, so a wave starts on the first row of
-// its tile while the other row loads are still in flight (fdct_tile needs all
-// eight rows before its first FMA: chain by chain, each chain reads every
-// row).  sched_barrier keeps hipcc from hoisting the later rows' converts
-// (and their load waits) above the earlier rows' FMAs.
-template <typename TS, typename RowOf, typename Emit>
-__device__ __forceinline__ void fdct_tile_rows_first(const TS& T, RowOf&& row_of, Emit&& emit) {
-    float p[8][8];
-    unroll<8>([&](auto i) {
-        float xr[8];
-        row_of(i, xr);
-        unroll<8>([&](auto v) {
-            unroll<8>([&](auto col) {
-                p[v][col] = T.template mac<v * 8 + i>(xr[col], i == 0 ? 0.0f : p[v][col]);
-            });
-        });
-        __builtin_amdgcn_sched_barrier(0);
-    });
-    unroll<8>([&](auto v) {
-        float c[8];
-        unroll<8>([&](auto u) {
-            float s = 0.0f;
-            unroll<8>([&](auto k) { s = T.template mac<u * 8 + k>(p[v][k], s); });
-            c[u] = s;
-        });
-        emit(v, c);
-    });
-}
-
 // cublasDCTv2 pass order (main_cublass_2.cu:228-235): R = X.T^T (row pass,
 // temp1) first, then C = T.R, each a sequential FMA chain over the 8
 // non-trivial terms of the block-diagonal GEMM's k range.

@@ -175,24 +175,6 @@ int main(int argc, char** argv) {
         {"bandi8", "fwd u8->i8 band 8 w/cu b256", band_fwd<int8_t, (I8 & ~(3u << 12)), 8>, 2, 1, true},
         {"bandi8", "fwd u8->i8 band 16 w/cu b512", band_fwd<int8_t, I8, 16>, 2, 1, true},
         {"bandi8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
-        // first pass issued row by row (consume each input row as it lands)
-        {"rows", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
-        {"rows", "fwd u8->f32 rows first", prod_f32_fwd<P | kVarRowsFirst>, 5, 4, true},
-        {"rows", "fwd u8->f32 library again", prod_f32_fwd<P>, 5, 4, true},
-        {"rows", "fwd u8->f32 rows first again", prod_f32_fwd<P | kVarRowsFirst>, 5, 4, true},
-        {"rowsi8", "fwd u8->i8 library", prod_i8_fwd<I8>, 2, 1, true},
-        {"rowsi8", "fwd u8->i8 rows first", prod_i8_fwd<I8 | kVarRowsFirst>, 2, 1, true},
-        {"rowsi8", "fwd u8->i8 library again", prod_i8_fwd<I8>, 2, 1, true},
-        {"rowsi8", "fwd u8->i8 rows first again", prod_i8_fwd<I8 | kVarRowsFirst>, 2, 1, true},
-        // fused quantiser trunc(fma(C, r, +-0.49999997)) (kVarFusedQ; exact only for verified divisors)
-        {"fq", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
-        {"fq", "fwd u8->f32 fused quantiser", prod_f32_fwd<P | kVarFusedQ>, 5, 4, true},
-        {"fq", "fwd u8->f32 library again", prod_f32_fwd<P>, 5, 4, true},
-        {"fq", "fwd u8->f32 fused quantiser again", prod_f32_fwd<P | kVarFusedQ>, 5, 4, true},
-        {"fqi8", "fwd u8->i8 library", prod_i8_fwd<I8>, 2, 1, true},
-        {"fqi8", "fwd u8->i8 fused quantiser", prod_i8_fwd<I8 | kVarFusedQ>, 2, 1, true},
-        {"fqi8", "fwd u8->i8 library again", prod_i8_fwd<I8>, 2, 1, true},
-        {"fqi8", "fwd u8->i8 fused quantiser again", prod_i8_fwd<I8 | kVarFusedQ>, 2, 1, true},
         {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
         {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},
