@@ -48,9 +48,13 @@ static int run_sharded(size_t n, int ngpus, bool int8, long runs) {
     std::vector<hpdct_comm> comms(ngpus);
     CHECK_HPDCT(hpdct_comm_init_all(comms.data(), ngpus, devs.data()));
 
+    // every device rotates over enough slab copies that its inputs total >= 1 GiB,
+    // 4x the 256 MiB Infinity Cache: each timed forward then reads HBM, not the
+    // cache (at 8 GPUs a 16384^2 slab is 32 MiB)
+    constexpr size_t kRotateBytes = size_t(1) << 30;
     struct Dev {
         hipStream_t s;
-        uint8_t* slab;
+        std::vector<uint8_t*> slab;  // identical copies, rotated
         void* coef;
         int64_t first, rows;
         hipEvent_t e0, e1, e2;
@@ -62,13 +66,15 @@ static int run_sharded(size_t n, int ngpus, bool int8, long runs) {
         CHECK_HIP(hipSetDevice(d));
         CHECK_HIP(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
         CHECK_HPDCT(hpdct_shard_rows(h, ngpus, d, &x.first, &x.rows));
-        CHECK_HIP(hipMalloc(&x.slab, (size_t)x.rows * n));
+        const size_t slab_bytes = (size_t)x.rows * n;
+        x.slab.resize(std::min<size_t>(64, (kRotateBytes + slab_bytes - 1) / slab_bytes));
+        for (uint8_t*& p : x.slab) CHECK_HIP(hipMalloc(&p, slab_bytes));
         CHECK_HIP(hipMalloc(&x.coef, (size_t)x.rows * n * esz));
         if (d == 0) CHECK_HIP(hipMalloc(&frame, n * n * esz));
         CHECK_HIP(hipEventCreate(&x.e0));
         CHECK_HIP(hipEventCreate(&x.e1));
         CHECK_HIP(hipEventCreate(&x.e2));
-        CHECK_HPDCT(hpdct_fill_hash_u8(x.slab, x.rows * w, 42, x.first * w, x.s));
+        for (uint8_t* p : x.slab) CHECK_HPDCT(hpdct_fill_hash_u8(p, x.rows * w, 42, x.first * w, x.s));
     }
     float best_c = 1e30f, best_g = 1e30f;
     for (long r = 0; r < (runs > 0 ? runs : 1); ++r) {
@@ -76,7 +82,8 @@ static int run_sharded(size_t n, int ngpus, bool int8, long runs) {
             CHECK_HIP(hipSetDevice(d));
             CHECK_HIP(hipStreamSynchronize(dv[d].s));
             CHECK_HIP(hipEventRecord(dv[d].e0, dv[d].s));
-            CHECK_HPDCT(hpdct_forward_slab(comms[d], dv[d].slab, dv[d].coef, ot, h, w, dv[d].s));
+            CHECK_HPDCT(hpdct_forward_slab(comms[d], dv[d].slab[r % dv[d].slab.size()], dv[d].coef, ot, h, w,
+                                           dv[d].s));
             CHECK_HIP(hipEventRecord(dv[d].e1, dv[d].s));
         }
         CHECK_HPDCT(hpdct_group_start());
@@ -99,15 +106,17 @@ static int run_sharded(size_t n, int ngpus, bool int8, long runs) {
     }
     // one GPU, whole frame, on device 0: the reference for bit-exactness and speedup
     CHECK_HIP(hipSetDevice(0));
-    uint8_t* full_in = nullptr;
+    std::vector<uint8_t*> full_in(std::min<size_t>(64, (kRotateBytes + n * n - 1) / (n * n)));
     void* full_out = nullptr;
-    CHECK_HIP(hipMalloc(&full_in, n * n));
+    for (uint8_t*& p : full_in) {
+        CHECK_HIP(hipMalloc(&p, n * n));
+        CHECK_HPDCT(hpdct_fill_hash_u8(p, h * w, 42, 0, dv[0].s));
+    }
     CHECK_HIP(hipMalloc(&full_out, n * n * esz));
-    CHECK_HPDCT(hpdct_fill_hash_u8(full_in, h * w, 42, 0, dv[0].s));
     float best_one = 1e30f;
     for (long r = 0; r < (runs > 0 ? runs : 1) + 1; ++r) {
         CHECK_HIP(hipEventRecord(dv[0].e0, dv[0].s));
-        CHECK_HPDCT(hpdct_forward(full_in, HPDCT_U8, full_out, ot, h, w, nullptr, 0u, dv[0].s));
+        CHECK_HPDCT(hpdct_forward(full_in[r % full_in.size()], HPDCT_U8, full_out, ot, h, w, nullptr, 0u, dv[0].s));
         CHECK_HIP(hipEventRecord(dv[0].e1, dv[0].s));
         CHECK_HIP(hipEventSynchronize(dv[0].e1));
         float ms = 0.0f;
@@ -120,11 +129,11 @@ static int run_sharded(size_t n, int ngpus, bool int8, long runs) {
     const bool same = memcmp(a.data(), b.data(), a.size()) == 0;
     printf("SHARD (%zu,%zu) x %d %s: compute %f ms, gather %f ms, one-GPU %f ms, compute speedup %.2f, bit-exact %s\n",
            n, n, ngpus, int8 ? "int8" : "fp32", best_c, best_g, best_one, best_one / best_c, same ? "yes" : "NO");
-    CHECK_HIP(hipFree(full_in));
+    for (uint8_t* p : full_in) CHECK_HIP(hipFree(p));
     CHECK_HIP(hipFree(full_out));
     for (int d = 0; d < ngpus; ++d) {
         CHECK_HIP(hipSetDevice(d));
-        CHECK_HIP(hipFree(dv[d].slab));
+        for (uint8_t* p : dv[d].slab) CHECK_HIP(hipFree(p));
         CHECK_HIP(hipFree(dv[d].coef));
         CHECK_HIP(hipEventDestroy(dv[d].e0));
         CHECK_HIP(hipEventDestroy(dv[d].e1));

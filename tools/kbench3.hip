@@ -175,6 +175,9 @@ int main(int argc, char** argv) {
         {"bandi8", "fwd u8->i8 band 8 w/cu b256", band_fwd<int8_t, (I8 & ~(3u << 12)), 8>, 2, 1, true},
         {"bandi8", "fwd u8->i8 band 16 w/cu b512", band_fwd<int8_t, I8, 16>, 2, 1, true},
         {"bandi8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        // the two library forward kernels alone (frame-size sweeps: kbench3 HxW 64 3 libf32 / libi8)
+        {"libf32", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
+        {"libi8", "fwd u8->i8 library", prod_i8_fwd<I8>, 2, 1, true},
         {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
         {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},

@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/bench_$ctr" -o run -- \
-        python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-c4c5 > "$OUT/bench_$ctr.log" 2>&1 || exit $?
+        python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-c4c5 --sustain-s 0 > "$OUT/bench_$ctr.log" 2>&1 || exit $?
     timeout -k 10 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/calib_$ctr" -o run -- \
         "$ROOT/tools/membench" calib > "$OUT/calib_$ctr.log" 2>&1 || exit $?
 done
