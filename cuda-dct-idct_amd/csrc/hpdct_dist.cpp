@@ -92,11 +92,20 @@ hpdct_status hpdct_comm_init_all(hpdct_comm* comms, int ndev, const int* devices
         delete[] raw;
         return st;
     }
-    for (int i = 0; i < ndev; ++i) comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i]};
+    bool ok = true;
+    for (int i = 0; i < ndev; ++i) {
+        comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i]};
+        ok = ok && comms[i];
+    }
+    if (!ok) {  // all or nothing: no communicator survives a failed call
+        for (int i = 0; i < ndev; ++i) {
+            (void)ncclCommDestroy(raw[i]);
+            delete comms[i];
+            comms[i] = nullptr;
+        }
+    }
     delete[] raw;
-    for (int i = 0; i < ndev; ++i)
-        if (!comms[i]) return fail(HPDCT_ERROR_DEVICE, "out of host memory");
-    return HPDCT_SUCCESS;
+    return ok ? HPDCT_SUCCESS : fail(HPDCT_ERROR_DEVICE, "out of host memory");
 }
 
 hpdct_status hpdct_comm_unique_id(hpdct_unique_id* id) {

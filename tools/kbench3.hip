@@ -19,6 +19,7 @@
 #include "hpdct_launch.hpp"
 #include "kbench_dma.hpp"
 #include "kbench_band.hpp"
+#include "kbench_spec.hpp"
 
 using namespace hpdct;
 
@@ -75,6 +76,17 @@ void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+// wave-specialised: 4 store waves + kCompute compute waves per CU (kbench_spec.hpp)
+template <uint32_t kCompute, bool kMath, uint32_t kSleep>
+void spec_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (!spec::spec_ok(c.g)) {
+        fprintf(stderr, "spec: width must be a multiple of 512 px\n");
+        exit(2);
+    }
+    (void)spec::spec_go<kCompute, kMath, kSleep, kVarFastDiv>(static_cast<const uint8_t*>(in),
+                                                              static_cast<float*>(out), c.g, c.qp, c.cus, s);
 }
 
 // ---- access-pattern probes (no arithmetic; values are not a transform) ----
@@ -178,6 +190,16 @@ int main(int argc, char** argv) {
         // the two library forward kernels alone (frame-size sweeps: kbench3 HxW 64 3 libf32 / libi8)
         {"libf32", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
         {"libi8", "fwd u8->i8 library", prod_i8_fwd<I8>, 2, 1, true},
+        {"spec", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
+        {"spec", "fwd u8->f32 spec 4 store + 12 compute", spec_fwd<12, true, 0>, 5, 4, true},
+        {"spec", "fwd u8->f32 spec 4 store + 8 compute", spec_fwd<8, true, 0>, 5, 4, true},
+        {"spec", "fwd u8->f32 library again", prod_f32_fwd<P>, 5, 4, true},
+        {"spec", "fwd u8->f32 spec 4 store + 12 compute again", spec_fwd<12, true, 0>, 5, 4, true},
+        {"specpat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
+        {"specpat", "spec pattern 4+12, no compute", spec_fwd<12, false, 0>, 5, 4, false},
+        {"specpat", "spec pattern 4+12, sleep 40x64 cyc per set", spec_fwd<12, false, 40>, 5, 4, false},
+        {"specpat", "spec pattern 4+8, sleep 40x64 cyc per set", spec_fwd<8, false, 40>, 5, 4, false},
+        {"specpat", "pat one set per wave (grid) again", pat_grid_go, 5, 4, false},
         {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
         {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},
