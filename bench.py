@@ -131,6 +131,13 @@ def main():
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the ONE JSON line is the only thing this process writes to stdout: the
+    # libraries' own banners (RCCL prints its version block to stdout when a
+    # communicator is created) are sent to stderr by pointing fd 1 there; the
+    # line goes out through a duplicate of the original stdout
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     import hpdct
@@ -313,7 +320,7 @@ def main():
         result["cpu_baseline"] = _cpu_baseline(n)
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if use_pg:
         try:
             dist.destroy_process_group()
