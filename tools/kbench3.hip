@@ -20,6 +20,7 @@
 #include "kbench_dma.hpp"
 #include "kbench_band.hpp"
 #include "kbench_spec.hpp"
+#include "kbench_rtpk.hpp"
 
 using namespace hpdct;
 
@@ -66,9 +67,9 @@ void dma_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
 }
 
 // banded persistent schedule with register prefetch (kbench_band.hpp)
-template <typename TOut, unsigned kVar, uint32_t kWavesPerCU>
+template <typename TOut, unsigned kVar, uint32_t kWavesPerCU, bool kPk = false>
 void band_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    (void)band::band_go<TOut, kVar>(static_cast<const uint8_t*>(in), static_cast<TOut*>(out), c.g, c.qp, c.cus,
+    (void)band::band_go<TOut, kVar, kPk>(static_cast<const uint8_t*>(in), static_cast<TOut*>(out), c.g, c.qp, c.cus,
                                     kWavesPerCU, s);
 }
 template <unsigned kVar>
@@ -76,6 +77,37 @@ void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>),
                        grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), 0, s,
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+// the tools-only tile kernel (kbench_variants.hpp), e.g. with ab::kVarPacked
+template <typename TOut, unsigned kVar>
+void ab_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::ab::fdct_kernel<uint8_t, TOut, true, true, false, kVar>),
+                       grid_for(c.g, false, c.cus, ab::kBlock<kVar>), dim3(ab::kBlock<kVar>), 0, s,
+                       static_cast<const uint8_t*>(in), static_cast<TOut*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+
+// ---- C3 round trip, u8 reconstruction into `out`, coefficients into g_coef[set]
+std::vector<uint8_t*> g_img;
+std::vector<float*> g_coef;
+RtSums* g_sums = nullptr;
+int set_of(const void* in) {
+    for (size_t i = 0; i < g_img.size(); ++i)
+        if (g_img[i] == in) return (int)i;
+    return 0;
+}
+template <bool kStats>
+void rt_prod(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, true, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+                       static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
+}
+template <bool kStats>
+void rt_pk(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((rtpk::roundtrip_pk_kernel<kStats>), roundtrip_grid(c.g), dim3(512), 0, s,
+                       static_cast<const uint8_t*>(in), g_coef[set_of(in)], static_cast<uint8_t*>(out),
+                       kStats ? g_sums : nullptr, c.g, c.qp);
 }
 
 // wave-specialised: 4 store waves + kCompute compute waves per CU (kbench_spec.hpp)
@@ -87,6 +119,41 @@ void spec_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
     }
     (void)spec::spec_go<kCompute, kMath, kSleep, kVarFastDiv>(static_cast<const uint8_t*>(in),
                                                               static_cast<float*>(out), c.g, c.qp, c.cus, s);
+}
+
+// ---- VALU issue probe: kWaves waves per CU, each kChains independent fma
+// chains of kIters steps (scalar v_fma_f32, or packed v_pk_fma_f32 doing two
+// fmas per instruction); inline asm so the compiler neither packs the scalar
+// form nor unpacks the packed one.  Same fma count in both forms.
+template <bool kPk, uint32_t kChains>
+__global__ __launch_bounds__(256) void issue_probe(float* out, uint32_t iters, float a) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float acc = 0.0f;
+    if constexpr (kPk) {
+        f2 s[kChains];
+        const f2 m = {a, a};
+        unroll<kChains>([&](auto k) { s[k] = f2{(float)threadIdx.x + k, (float)k}; });
+        for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+            for (uint32_t k = 0; k < kChains; ++k) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(s[k]) : "v"(m));
+        }
+        unroll<kChains>([&](auto k) { acc += s[k].x + s[k].y; });
+    } else {
+        float s[2 * kChains];
+        unroll<2 * kChains>([&](auto k) { s[k] = (float)threadIdx.x + k; });
+        for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+            for (uint32_t k = 0; k < 2 * kChains; ++k) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(s[k]) : "v"(a));
+        }
+        unroll<2 * kChains>([&](auto k) { acc += s[k]; });
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+// bpp is unused for these (no pixels); the printed "frac" column is meaningless
+template <bool kPk, uint32_t kWavesPerCU>
+void issue_go(const void*, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((issue_probe<kPk, 8>), dim3(c.cus * kWavesPerCU / 4u), dim3(256), 0, s, static_cast<float*>(out),
+                       4096u, 0.999f);
 }
 
 // ---- access-pattern probes (no arithmetic; values are not a transform) ----
@@ -187,6 +254,36 @@ int main(int argc, char** argv) {
         {"bandi8", "fwd u8->i8 band 8 w/cu b256", band_fwd<int8_t, (I8 & ~(3u << 12)), 8>, 2, 1, true},
         {"bandi8", "fwd u8->i8 band 16 w/cu b512", band_fwd<int8_t, I8, 16>, 2, 1, true},
         {"bandi8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"bandpk", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"bandpk", "fwd u8->f32 band 4 w/cu", band_fwd<float, (P & ~(3u << 12)), 4>, 5, 4, true},
+        {"bandpk", "fwd u8->f32 band 4 w/cu packed", band_fwd<float, (P & ~(3u << 12)), 4, true>, 5, 4, true},
+        {"bandpk", "fwd u8->f32 band 8 w/cu b256 packed", band_fwd<float, (P & ~(3u << 12)), 8, true>, 5, 4, true},
+        {"bandpk", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"bandpk", "fwd u8->f32 band 4 w/cu packed again", band_fwd<float, (P & ~(3u << 12)), 4, true>, 5, 4, true},
+        {"pk", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"pk", "fwd u8->f32 packed (b512)", ab_fwd<float, P | ab::kVarPacked>, 5, 4, true},
+        {"pk", "fwd u8->f32 packed (b256)", ab_fwd<float, (P & ~(3u << 12)) | ab::kVarPacked>, 5, 4, true},
+        {"pk", "fwd u8->f32 packed (b1024)", ab_fwd<float, P | (3u << 12) | ab::kVarPacked>, 5, 4, true},
+        {"pk", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"pk", "fwd u8->f32 packed (b512) again", ab_fwd<float, P | ab::kVarPacked>, 5, 4, true},
+        {"rtpk", "rt + sums, library", rt_prod<true>, 6, 1, true},
+        {"rtpk", "rt + sums, packed", rt_pk<true>, 6, 1, true},
+        {"rtpk", "rt no sums, library", rt_prod<false>, 6, 1, true},
+        {"rtpk", "rt no sums, packed", rt_pk<false>, 6, 1, true},
+        {"rtpk", "rt + sums, library again", rt_prod<true>, 6, 1, true},
+        {"rtpk", "rt + sums, packed again", rt_pk<true>, 6, 1, true},
+        {"pki8", "fwd u8->i8 library (b512)", prod_i8_fwd<I8>, 2, 1, true},
+        {"pki8", "fwd u8->i8 packed (b512)", ab_fwd<int8_t, I8 | ab::kVarPacked>, 2, 1, true},
+        {"pki8", "fwd u8->i8 packed (b256)", ab_fwd<int8_t, (I8 & ~(3u << 12)) | ab::kVarPacked>, 2, 1, true},
+        {"pki8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"pki8", "fwd u8->i8 packed (b512) again", ab_fwd<int8_t, I8 | ab::kVarPacked>, 2, 1, true},
+        // 8 chains x 4096 steps x 2 fmas per lane pair: 65,536 fma per lane in both forms
+        {"issue", "valu scalar fma, 4 waves/cu", issue_go<false, 4>, 0, 4, false},
+        {"issue", "valu packed fma, 4 waves/cu", issue_go<true, 4>, 0, 4, false},
+        {"issue", "valu scalar fma, 8 waves/cu", issue_go<false, 8>, 0, 4, false},
+        {"issue", "valu packed fma, 8 waves/cu", issue_go<true, 8>, 0, 4, false},
+        {"issue", "valu scalar fma, 16 waves/cu", issue_go<false, 16>, 0, 4, false},
+        {"issue", "valu packed fma, 16 waves/cu", issue_go<true, 16>, 0, 4, false},
         // the two library forward kernels alone (frame-size sweeps: kbench3 HxW 64 3 libf32 / libi8)
         {"libf32", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
         {"libi8", "fwd u8->i8 library", prod_i8_fwd<I8>, 2, 1, true},
@@ -229,7 +326,33 @@ int main(int argc, char** argv) {
             CK(launch_fill_hash_impl(img[s], px, 1000u + s, 0, 0));
         }
     }
+    const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
+    if (want_rt) {
+        g_img = img;
+        g_coef.resize(nsets);
+        for (auto& p : g_coef) CK(hipMalloc(&p, px * 4));
+        CK(hipMalloc(&g_sums, sizeof(RtSums)));
+    }
     CK(hipDeviceSynchronize());
+    if (want_rt) {  // coefficients and sums of the packed round trip == the library's, set 1
+        std::vector<float> c0(px), c1(px);
+        RtSums s0, s1;
+        rt_prod<true>(img[1], out[2], c, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(c0.data(), g_coef[1], px * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&s0, g_sums, sizeof(s0), hipMemcpyDeviceToHost));
+        CK(hipMemset(g_coef[1], 0xa5, px * 4));
+        rt_pk<true>(img[1], out[2], c, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(c1.data(), g_coef[1], px * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&s1, g_sums, sizeof(s1), hipMemcpyDeviceToHost));
+        const bool cok = memcmp(c0.data(), c1.data(), px * 4) == 0;
+        const bool sok = memcmp(&s0, &s1, sizeof(s0)) == 0;
+        printf("check rt packed coefficients %s, sums %s (sse_u8 %llu sum_x2 %llu sse_f32_fx %llu)\n",
+               cok ? "bit-exact" : "MISMATCH", sok ? "identical" : "DIFFER", (unsigned long long)s1.sse_u8,
+               (unsigned long long)s1.sum_x2, (unsigned long long)s1.sse_f32_fx);
+        if (!cok || !sok) return 1;
+    }
     // correctness: each variant against its group's first entry, on sets 0 and 1
     {
         std::vector<uint8_t> ref(px * 4), got(px * 4);

@@ -8,9 +8,14 @@
 // non-persistent wave (tools/kbench3 "pat" group, profiles/r03).
 // Arithmetic, staging and stores are the product's (fdct_tile, quantise,
 // RowSink), so the output is bit-identical.
+// kPk: the packed-fp32 transform and quotient of tools/kbench_variants.hpp
+// (ab::fdct_tile_pk, v_pk_fma_f32; bit-exact): at one wave per SIMD a wave
+// issues a VALU instruction every 4 cycles at best, so two fmas per
+// instruction may give back the rate the band schedule loses there.
 #pragma once
 
 #include "hpdct_kernels_impl.hpp"
+#include "kbench_variants.hpp"
 
 namespace hpdct {
 namespace band {
@@ -46,13 +51,39 @@ __device__ __forceinline__ void walk_band(const TIn* __restrict__ src, const Til
     }
 }
 
-template <typename TOut, unsigned kVar>
+template <typename TOut, unsigned kVar, bool kPk = false>
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_band_kernel(const uint8_t* __restrict__ img,
                                                                    TOut* __restrict__ out, TileGrid g, QParams qp) {
     const TSource<true, true> T(nullptr);
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, TOut> sink{out, g.width, slots};
     walk_band<kVar>(img, g, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
+        if constexpr (kPk) {
+            static_assert(std::is_same_v<TOut, float> && (kVar & kVarFastDiv) != 0, "packed: fp32 out, fast quotient");
+            using ab::f32x2;
+            float xs[8][8];
+            raw.to_float(xs, 0.0f);
+            f32x2 x2[8][4];
+            unroll<8>([&](auto i) {
+                unroll<4>([&](auto cp) { x2[i][cp] = f32x2{xs[i][2 * cp], xs[i][2 * cp + 1]} - f32x2{128.0f, 128.0f}; });
+            });
+            ab::fdct_tile_pk(x2, [&](auto v, f32x2(&c2)[4]) {
+                float c[8];
+                unroll<4>([&](auto k) {
+                    constexpr int u0 = ab::kPairU[k][0], u1 = ab::kPairU[k][1];
+                    const f32x2 q2 = {qp.q.v[v * 8 + u0], qp.q.v[v * 8 + u1]};
+                    const f32x2 r2 = {qp.r.v[v * 8 + u0], qp.r.v[v * 8 + u1]};
+                    const f32x2 q0 = c2[k] * r2;
+                    const f32x2 e = ab::fma2(-q0, q2, c2[k]);
+                    f32x2 d = ab::fma2(e, r2, q0);
+                    d = d + f32x2{__builtin_copysignf(0.49999997f, d.x), __builtin_copysignf(0.49999997f, d.y)};
+                    c[u0] = __builtin_truncf(d.x);
+                    c[u1] = __builtin_truncf(d.y);
+                });
+                sink(v, p, ok, seg, c);
+            });
+            return;
+        }
         float x[8][8];
         raw.to_float(x, 128.0f);
         fdct_tile(T, x, [&](auto v, float (&c)[8]) {
@@ -69,12 +100,12 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_band_kernel(const uint8_
 }
 
 // waves_per_cu resident waves per CU (the grid), kVar's workgroup size
-template <typename TOut, unsigned kVar>
+template <typename TOut, unsigned kVar, bool kPk = false>
 hipError_t band_go(const uint8_t* img, TOut* out, const TileGrid& g, const QParams& qp, uint32_t cus,
                    uint32_t waves_per_cu, hipStream_t s) {
     const uint32_t per = kBlock<kVar> / 64u, sets = (g.ntiles + 63u) / 64u;
     const uint32_t grid = std::min<uint32_t>((sets + per - 1) / per, cus * waves_per_cu / per);
-    hipLaunchKernelGGL((fdct_band_kernel<TOut, kVar>), dim3(grid), dim3(kBlock<kVar>), 0, s, img, out, g, qp);
+    hipLaunchKernelGGL((fdct_band_kernel<TOut, kVar, kPk>), dim3(grid), dim3(kBlock<kVar>), 0, s, img, out, g, qp);
     return hipGetLastError();
 }
 
