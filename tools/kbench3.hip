@@ -90,6 +90,7 @@ void ab_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
 // ---- C3 round trip, u8 reconstruction into `out`, coefficients into g_coef[set]
 std::vector<uint8_t*> g_img;
 std::vector<float*> g_coef;
+std::vector<float*> g_shift;  // drop-in forward's X-128 write-back planes
 RtSums* g_sums = nullptr;
 int set_of(const void* in) {
     for (size_t i = 0; i < g_img.size(); ++i)
@@ -208,6 +209,85 @@ void pat_grid_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        static_cast<float*>(out), c.g, nsets);
 }
 
+// ---- occupancy caps through dynamic LDS (round 3, session 3): kWg workgroups
+// per CU at most, so a 256-thread workgroup gives 4 x kWg waves per CU.  The
+// kernels do not use the dynamic part; it only reserves LDS.
+inline size_t cap_dyn_lds(uint32_t wg_per_cu, size_t static_bytes) {
+    size_t per = (160u * 1024u) / wg_per_cu;
+    per &= ~static_cast<size_t>(511);
+    return per > static_bytes ? per - static_bytes : 0;
+}
+// dynamic LDS bytes that leave room for at most kWg workgroups of `kern` per CU
+template <typename K>
+size_t cap_for(K kern, uint32_t wg_per_cu) {
+    hipFuncAttributes a{};
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kern));
+    const size_t dyn = cap_dyn_lds(wg_per_cu, a.sharedSizeBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(dyn));
+    return dyn;
+}
+// the headline's access pattern (no arithmetic), one set per wave, capped
+template <uint32_t kWg>
+void pat_grid_cap_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t nsets = c.g.ntiles / 64u;
+    static const size_t dyn = cap_for(pat_band<false>, kWg);
+    hipLaunchKernelGGL((pat_band<false>), dim3(nsets / 4u), dim3(256), dyn, s, static_cast<const uint8_t*>(in),
+                       static_cast<float*>(out), c.g, nsets);
+}
+// the tools-only tile kernel (scalar or packed) with kWg workgroups per CU at most
+template <typename TOut, unsigned kVar, uint32_t kWg>
+void ab_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    constexpr uint32_t kB = ab::kBlock<kVar>;
+    auto* k = hpdct::ab::fdct_kernel<uint8_t, TOut, true, true, false, kVar>;
+    static const size_t dyn = cap_for(k, kWg);
+    hipLaunchKernelGGL(k, grid_for(c.g, false, c.cus, kB), dim3(kB), dyn, s, static_cast<const uint8_t*>(in),
+                       static_cast<TOut*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+// the library's headline kernel itself, capped
+template <unsigned kVar, uint32_t kWg>
+void prod_f32_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = hpdct::fdct_kernel<uint8_t, float, true, true, false, kVar>;
+    static const size_t dyn = cap_for(k, kWg);
+    hipLaunchKernelGGL(k, grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s,
+                       static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+// C3 round trip (512-thread workgroups), capped at kWg workgroups per CU (0: uncapped)
+template <bool kStats, uint32_t kWg>
+void rt_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = roundtrip_kernel<kRtReconU8, kStats, true, 2, false>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL(k, roundtrip_grid(c.g), dim3(512), dyn, s, static_cast<const uint8_t*>(in), g_coef[set_of(in)],
+                       out, kStats ? g_sums : nullptr, c.g, c.qp);
+}
+// fp32 inverse (duo mapping, built-in T, dequantise), coefficients from g_coef, capped (0: uncapped)
+template <uint32_t kWg>
+void inv_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = idct_duo_kernel<true, true, kDuoVar, float>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    hipLaunchKernelGGL(k, duo_grid(c.g, kBlock<kDuoVar>), dim3(kBlock<kDuoVar>), dyn, s, g_coef[set_of(in)],
+                       static_cast<float*>(out), nullptr, c.g, nullptr, c.qp.q, 128.0f);
+}
+
+// fp32 inverse, duo mapping with a chosen block size (kVar bits 12..13), capped (0: uncapped)
+template <unsigned kVar, uint32_t kWg>
+void inv_cap_v(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = idct_duo_kernel<true, true, kVar, float>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    hipLaunchKernelGGL(k, duo_grid(c.g, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s, g_coef[set_of(in)],
+                       static_cast<float*>(out), nullptr, c.g, nullptr, c.qp.q, 128.0f);
+}
+// the drop-in forward (fp32 in, built-in T here, X-128 written back into g_coef[set]), duo, capped
+template <unsigned kVar, uint32_t kWg>
+void dropin_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = fdct_duo_kernel<true, true, true, kVar>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    float* src = g_coef[set_of(in)];
+    hipLaunchKernelGGL(k, duo_grid(c.g, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s, src, static_cast<float*>(out),
+                       g_shift[set_of(in)], c.g, nullptr, c.qp, 128.0f);
+}
+
 int main(int argc, char** argv) {
     int n = 8192, hgt = 8192;
     if (argc > 1) {
@@ -297,6 +377,89 @@ int main(int argc, char** argv) {
         {"specpat", "spec pattern 4+12, sleep 40x64 cyc per set", spec_fwd<12, false, 40>, 5, 4, false},
         {"specpat", "spec pattern 4+8, sleep 40x64 cyc per set", spec_fwd<8, false, 40>, 5, 4, false},
         {"specpat", "pat one set per wave (grid) again", pat_grid_go, 5, 4, false},
+        // occupancy caps (dynamic LDS): does the one-set-per-wave dispatch gain DRAM efficiency with fewer
+        // waves per CU, as the banded schedule did (0.77 at 4 w/cu), and can the packed math keep up there?
+        {"occpat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
+        {"occpat", "pat grid cap 4 w/cu", pat_grid_cap_go<1>, 5, 4, false},
+        {"occpat", "pat grid cap 8 w/cu", pat_grid_cap_go<2>, 5, 4, false},
+        {"occpat", "pat grid cap 12 w/cu", pat_grid_cap_go<3>, 5, 4, false},
+        {"occpat", "pat grid cap 16 w/cu", pat_grid_cap_go<4>, 5, 4, false},
+        {"occpat", "pat grid cap 24 w/cu", pat_grid_cap_go<6>, 5, 4, false},
+        {"occpat", "pat one set per wave (grid) again", pat_grid_go, 5, 4, false},
+        {"occ", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"occ", "fwd u8->f32 scalar b256 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)), 2>, 5, 4, true},
+        {"occ", "fwd u8->f32 scalar b256 cap 12 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)), 3>, 5, 4, true},
+        {"occ", "fwd u8->f32 packed (b512)", ab_fwd<float, P | ab::kVarPacked>, 5, 4, true},
+        {"occ", "fwd u8->f32 packed b256 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | ab::kVarPacked, 2>, 5, 4, true},
+        {"occ", "fwd u8->f32 packed b256 cap 12 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | ab::kVarPacked, 3>, 5, 4, true},
+        {"occ", "fwd u8->f32 packed b512 cap 8 w/cu", ab_fwd_cap<float, P | ab::kVarPacked, 1>, 5, 4, true},
+        {"occ", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"occ", "fwd u8->f32 packed b256 cap 12 w/cu again", ab_fwd_cap<float, (P & ~(3u << 12)) | ab::kVarPacked, 3>, 5, 4, true},
+        // round 3, session 3: finer occupancy caps (64-thread workgroups = one wave each)
+        {"occ2", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b256 cap 12 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)), 3>, 5, 4, true},
+        {"occ2", "fwd u8->f32 library kernel b512 cap 8 w/cu", prod_f32_fwd_cap<P, 1>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b64 cap 6 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 6>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b64 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 8>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b64 cap 10 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 10>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b64 cap 12 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 12>, 5, 4, true},
+        {"occ2", "fwd u8->f32 packed b64 cap 6 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 6>, 5, 4, true},
+        {"occ2", "fwd u8->f32 packed b64 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 8>, 5, 4, true},
+        {"occ2", "fwd u8->f32 packed b256 cap 4 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | ab::kVarPacked, 1>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b256 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)), 2>, 5, 4, true},
+        {"occ2", "fwd u8->f32 library (b512) again", prod_f32_fwd<P>, 5, 4, true},
+        {"occ2", "fwd u8->f32 scalar b256 cap 12 w/cu again", ab_fwd_cap<float, (P & ~(3u << 12)), 3>, 5, 4, true},
+        {"occi8", "fwd u8->i8 library (b512)", prod_i8_fwd<I8>, 2, 1, true},
+        {"occi8", "fwd u8->i8 scalar b256 cap 12 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)), 3>, 2, 1, true},
+        {"occi8", "fwd u8->i8 scalar b256 cap 16 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)), 4>, 2, 1, true},
+        {"occi8", "fwd u8->i8 packed b256 cap 12 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)) | ab::kVarPacked, 3>, 2, 1, true},
+        {"occi8", "fwd u8->i8 packed b256 cap 8 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)) | ab::kVarPacked, 2>, 2, 1, true},
+        {"occi8", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"rtocc", "rt + sums, library", rt_cap<true, 0>, 6, 1, true},
+        {"rtocc", "rt + sums, cap 8 w/cu", rt_cap<true, 1>, 6, 1, true},
+        {"rtocc", "rt no sums, library", rt_cap<false, 0>, 6, 1, true},
+        {"rtocc", "rt no sums, cap 8 w/cu", rt_cap<false, 1>, 6, 1, true},
+        {"rtocc", "rt + sums, library again", rt_cap<true, 0>, 6, 1, true},
+        {"invocc", "inv f32->f32 duo library", inv_cap<0>, 8, 4, true},
+        {"invocc", "inv f32->f32 duo cap 8 w/cu", inv_cap<2>, 8, 4, true},
+        {"invocc", "inv f32->f32 duo cap 12 w/cu", inv_cap<3>, 8, 4, true},
+        {"invocc", "inv f32->f32 duo cap 16 w/cu", inv_cap<4>, 8, 4, true},
+        {"invocc", "inv f32->f32 duo cap 24 w/cu", inv_cap<6>, 8, 4, true},
+        {"invocc", "inv f32->f32 duo library again", inv_cap<0>, 8, 4, true},
+        // round 3, session 3: 1-wave workgroups, occupancy caps (sweep; also run at other frame sizes)
+        {"occsz", "fwd u8->f32 library", prod_f32_fwd<P>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 uncapped", ab_fwd<float, (P & ~(3u << 12)) | (1u << 12)>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 8>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 9 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 9>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 10 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 10>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 11 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 11>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 12 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 12>, 5, 4, true},
+        {"occsz", "fwd u8->f32 packed b64 cap 8 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 8>, 5, 4, true},
+        {"occsz", "fwd u8->f32 packed b64 cap 10 w/cu", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 10>, 5, 4, true},
+        {"occsz", "fwd u8->f32 library again", prod_f32_fwd<P>, 5, 4, true},
+        {"occsz", "fwd u8->f32 scalar b64 cap 10 w/cu again", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12), 10>, 5, 4, true},
+        {"occsz", "fwd u8->f32 packed b64 cap 8 w/cu again", ab_fwd_cap<float, (P & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 8>, 5, 4, true},
+        {"occi8b", "fwd u8->i8 library (b512)", prod_i8_fwd<I8>, 2, 1, true},
+        {"occi8b", "fwd u8->i8 scalar b64 uncapped", ab_fwd<int8_t, (I8 & ~(3u << 12)) | (1u << 12)>, 2, 1, true},
+        {"occi8b", "fwd u8->i8 scalar b64 cap 12 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)) | (1u << 12), 12>, 2, 1, true},
+        {"occi8b", "fwd u8->i8 scalar b64 cap 16 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)) | (1u << 12), 16>, 2, 1, true},
+        {"occi8b", "fwd u8->i8 packed b64 cap 16 w/cu", ab_fwd_cap<int8_t, (I8 & ~(3u << 12)) | (1u << 12) | ab::kVarPacked, 16>, 2, 1, true},
+        {"occi8b", "fwd u8->i8 library (b512) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"invb", "inv f32->f32 duo library", inv_cap<0>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b256 cap 8 w/cu", inv_cap<2>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b256 cap 12 w/cu", inv_cap<3>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b64 uncapped", inv_cap_v<kDuoVar | (1u << 12), 0>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b64 cap 8 w/cu", inv_cap_v<kDuoVar | (1u << 12), 8>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b64 cap 10 w/cu", inv_cap_v<kDuoVar | (1u << 12), 10>, 8, 4, true},
+        {"invb", "inv f32->f32 duo b64 cap 12 w/cu", inv_cap_v<kDuoVar | (1u << 12), 12>, 8, 4, true},
+        {"invb", "inv f32->f32 duo library again", inv_cap<0>, 8, 4, true},
+        {"dropin", "dropin fwd f32 duo library", dropin_fwd_cap<kDuoVar, 0>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo b256 cap 8 w/cu", dropin_fwd_cap<kDuoVar, 2>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo b256 cap 12 w/cu", dropin_fwd_cap<kDuoVar, 3>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo b64 cap 8 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 8>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo b64 cap 10 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 10>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo b64 cap 12 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 12>, 12, 4, true},
+        {"dropin", "dropin fwd f32 duo library again", dropin_fwd_cap<kDuoVar, 0>, 12, 4, true},
         {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
         {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},
@@ -327,11 +490,22 @@ int main(int argc, char** argv) {
         }
     }
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
-    if (want_rt) {
+    const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
+        return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
+               v.group == "dropin";
+    });
+    if (want_coef) {
         g_img = img;
         g_coef.resize(nsets);
         for (auto& p : g_coef) CK(hipMalloc(&p, px * 4));
+        if (std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "dropin"; })) {
+            g_shift.resize(nsets);
+            for (auto& p : g_shift) CK(hipMalloc(&p, px * 4));
+        }
         CK(hipMalloc(&g_sums, sizeof(RtSums)));
+        // the inverse's input: each set's quantised coefficients (the forward of its frame)
+        for (int k = 0; k < nsets; ++k) hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float> | kVarFastDiv>),
+                                                           grid_for(c.g, false, c.cus, 512), dim3(512), 0, 0, img[k], g_coef[k], nullptr, c.g, nullptr, c.qp, 128.0f);
     }
     CK(hipDeviceSynchronize());
     if (want_rt) {  // coefficients and sums of the packed round trip == the library's, set 1
