@@ -37,6 +37,8 @@ enum : unsigned {
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
+    kVarPacked = 1u << 19,    // uint8 -> fp32 quantised, built-in T: packed-fp32 transform and quotient
+                              // (fdct_tile_pk; 844 instead of 1,308 VALU instructions per set)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
     kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
@@ -446,6 +448,86 @@ __device__ __forceinline__ bool wave_tame(const float (&x)[8][8]) {
 // ---------------------------------------------------------------------------
 // Forward: image -> (quantised) coefficients.
 // ---------------------------------------------------------------------------
+// fdct_body's per-set work: level shift, transform, quantiser, row stores
+template <typename TIn, typename TOut, bool kQuant, bool kWriteback, unsigned kVar, typename TS, typename Sink,
+          typename WbSink>
+__device__ __forceinline__ void fdct_tile_body(const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg,
+                                               const TS& T, const Sink& sink, const WbSink& wb_sink,
+                                               TOut* __restrict__ out, const TileGrid& g, const QParams& qp,
+                                               float shift) {
+    float x[8][8];
+    raw.to_float(x, shift);
+    if constexpr (kWriteback) {
+        // the reference leaves X-128 in its input (main_newAppr.cu:273)
+        unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
+    }
+    auto emit = [&](auto v, float (&c)[8]) {
+        if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
+            unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+            const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
+            st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
+            return;
+        }
+        if constexpr (kQuant) {
+            unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+        }
+        sink(v, p, ok, seg, c);
+    };
+    if constexpr ((kVar & kVarRowFirst) != 0) {
+        fdct_tile_rowfirst(T, x, emit);
+    } else {
+        fdct_tile(T, x, emit);
+    }
+}
+
+// Packed-fp32 forward of uint8 pixels with the built-in T, quantised to fp32
+// (kVarPacked).  quot2(v, k, c2) returns the quotient pair of output columns
+// (pair_u(k, 0), pair_u(k, 1)) of row v.  The kernels define quot2 themselves
+// over their own QParams argument: handing the QParams to a device function
+// by reference made hipcc keep the quotient operands in scratch memory
+// (364 B per lane, 4x slower).
+template <unsigned kVar, typename Quot2>
+__device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img, float* __restrict__ out,
+                                                 const TileGrid& g, float shift, Quot2&& quot2) {
+    float4* const slots = wave_slots<kVar>();
+    const RowSink<kVar, float> sink{out, g.width, slots};
+    walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
+        float xs[8][8];
+        raw.to_float(xs, 0.0f);
+        f32x2 x2[8][4];  // X - 128, exact (integers)
+        unroll<8>([&](auto i) {
+            unroll<4>([&](auto cp) { x2[i][cp] = f32x2{xs[i][2 * cp], xs[i][2 * cp + 1]} - f32x2{shift, shift}; });
+        });
+        fdct_tile_pk(x2, [&](auto v, f32x2(&c2)[4]) {
+            float c[8];
+            unroll<4>([&](auto k) {
+                // round half away: trunc(d + copysign(0.49999997, d)) (verify_round3.c)
+                f32x2 d2 = quot2(v, k, c2[k]);
+                d2 = d2 + f32x2{__builtin_copysignf(0.49999997f, d2.x), __builtin_copysignf(0.49999997f, d2.y)};
+                c[pair_u(k, 0)] = __builtin_truncf(d2.x);
+                c[pair_u(k, 1)] = __builtin_truncf(d2.y);
+            });
+            sink(v, p, ok, seg, c);
+        });
+    });
+}
+
+// C / Q for one pair of output columns: the verified 3-op quotient per half,
+// or IEEE division (a generic lambda in each kernel, over its own QParams)
+#define HPDCT_PK_QUOT2(kVar, qp)                                                                   \
+    [&](auto v, auto k, f32x2 c2) -> f32x2 {                                                       \
+        constexpr int u0 = pair_u(k, 0), u1 = pair_u(k, 1);                                        \
+        const f32x2 q2 = {qp.q.v[v * 8 + u0], qp.q.v[v * 8 + u1]};                                 \
+        if constexpr (((kVar) & kVarFastDiv) != 0) {                                               \
+            const f32x2 r2 = {qp.r.v[v * 8 + u0], qp.r.v[v * 8 + u1]};                             \
+            const f32x2 q0 = c2 * r2;                                                              \
+            const f32x2 e = fma2(-q0, q2, c2);                                                     \
+            return fma2(e, r2, q0);                                                                \
+        } else {                                                                                   \
+            return f32x2{c2.x / q2.x, c2.y / q2.y};                                                \
+        }                                                                                          \
+    }
+
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback, unsigned kVar>
 __device__ __forceinline__ void fdct_body(const TIn* __restrict__ img, TOut* __restrict__ out,
                                           float* __restrict__ shifted, const TileGrid& g,
@@ -458,29 +540,7 @@ __device__ __forceinline__ void fdct_body(const TIn* __restrict__ img, TOut* __r
     const RowSink<kVar, float> wb_sink{shifted, g.width, slots};
 
     walk_sets<kVar>(img, g, slots, [&](const RawTile<TIn>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
-        float x[8][8];
-        raw.to_float(x, shift);
-        if constexpr (kWriteback) {
-            // the reference leaves X-128 in its input (main_newAppr.cu:273)
-            unroll<8>([&](auto i) { wb_sink(i, p, ok, seg, x[i]); });
-        }
-        auto emit = [&](auto v, float (&c)[8]) {
-            if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
-                unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
-                const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
-                st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
-                return;
-            }
-            if constexpr (kQuant) {
-                unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
-            }
-            sink(v, p, ok, seg, c);
-        };
-        if constexpr ((kVar & kVarRowFirst) != 0) {
-            fdct_tile_rowfirst(T, x, emit);
-        } else {
-            fdct_tile(T, x, emit);
-        }
+        fdct_tile_body<TIn, TOut, kQuant, kWriteback, kVar>(raw, p, ok, seg, T, sink, wb_sink, out, g, qp, shift);
     });
 }
 
@@ -488,7 +548,12 @@ template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteb
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
                                                             float* __restrict__ shifted, TileGrid g,
                                                             const float* __restrict__ t_dev, QParams qp, float shift) {
-    fdct_body<TIn, TOut, kQuant, kBuiltinT, kWriteback, kVar>(img, out, shifted, g, t_dev, qp, shift);
+    if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float> &&
+                  kBuiltinT && kQuant && !kWriteback && (kVar & kVarRowFirst) == 0) {
+        fdct_packed_body<kVar>(img, out, g, shift, HPDCT_PK_QUOT2(kVar, qp));
+    } else {
+        fdct_body<TIn, TOut, kQuant, kBuiltinT, kWriteback, kVar>(img, out, shifted, g, t_dev, qp, shift);
+    }
 }
 
 // A list of independent, equally sized uint8 frames in one launch
@@ -499,7 +564,11 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __rest
 template <typename TOut, unsigned kVar>
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_frames_kernel(FrameTable<TOut> ft, TileGrid g, QParams qp) {
     const uint32_t f = blockIdx.y;
-    fdct_body<uint8_t, TOut, true, true, false, kVar>(ft.in[f], ft.out[f], nullptr, g, nullptr, qp, 128.0f);
+    if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TOut, float>) {
+        fdct_packed_body<kVar>(ft.in[f], ft.out[f], g, 128.0f, HPDCT_PK_QUOT2(kVar, qp));
+    } else {
+        fdct_body<uint8_t, TOut, true, true, false, kVar>(ft.in[f], ft.out[f], nullptr, g, nullptr, qp, 128.0f);
+    }
 }
 
 // ---------------------------------------------------------------------------

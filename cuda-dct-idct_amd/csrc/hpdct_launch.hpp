@@ -28,6 +28,32 @@ inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t blo
     return dim3(blocks);
 }
 
+// Residency caps (round 3).  The DRAM serves the headline's mix of 1 B/px
+// reads and 4 B/px non-temporal writes best with few concurrent streams: its
+// access pattern alone runs at 0.72 of 8 TB/s with the hardware's default
+// residency and at 0.75-0.80 with 12-4 waves per CU (tools/kbench3 "occpat",
+// profiles/r03/m/).  The arithmetic needs more than one wave per SIMD to issue
+// at full rate, so the u8 -> fp32 tile kernel runs in one-wave workgroups with
+// at most kF32CapWavesPerCU resident per CU.  The cap is set by reserving
+// dynamic LDS the kernel does not use: gfx950 has 160 KiB per CU
+// (MI355X_MICROARCH.md), so a workgroup that holds more than 1/(k+1) of it
+// leaves room for at most k.
+constexpr size_t kLdsPerCU = 160u * 1024u;
+constexpr uint32_t kF32CapWavesPerCU = 10;
+
+// dynamic LDS bytes for at most `wgs` resident workgroups per CU of a kernel
+// that has `static_bytes` of its own (0 when no reservation is needed)
+inline size_t residency_cap_lds(size_t static_bytes, uint32_t wgs) {
+    if (wgs == 0) return 0;
+    const size_t per = (kLdsPerCU / wgs) & ~static_cast<size_t>(511);
+    return per > static_bytes ? per - static_bytes : 0;
+}
+template <typename K>
+size_t static_lds_of(K kern) {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kern)) == hipSuccess ? a.sharedSizeBytes : 0;
+}
+
 inline uint32_t device_cus() {
     static thread_local int cached_dev = -1;
     static thread_local uint32_t cached_cus = 256;
@@ -76,29 +102,48 @@ inline Mapping pick_mapping(const TileGrid& g, bool f32) {
     return f32 ? Mapping::kDuo : Mapping::kTile;
 }
 
+// cap_waves: at most that many resident waves per CU (0: the hardware's default)
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev, const QParams& q,
-                   float shift, hipStream_t s) {
-    hipLaunchKernelGGL((fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>), grid_for(g, false, 0, kBlock<kV>),
-                       dim3(kBlock<kV>), 0, s, img, out, shifted, g, t_dev, q, shift);
+                   float shift, hipStream_t s, uint32_t cap_waves = 0) {
+    auto* kern = fdct_kernel<TIn, TOut, kQuant, kBuiltinT, kWriteback, kV>;
+    size_t dyn = 0;
+    if (cap_waves != 0) {
+        static const size_t st = static_lds_of(kern);
+        dyn = residency_cap_lds(st, cap_waves / (kBlock<kV> / 64u));
+    }
+    hipLaunchKernelGGL(kern, grid_for(g, false, 0, kBlock<kV>), dim3(kBlock<kV>), dyn, s, img, out, shifted, g, t_dev,
+                       q, shift);
     return hipGetLastError();
 }
 
-// uint8 -> fp32 tile kernels: 1024-thread workgroups for frames of at most
-// kBigWgSetsPerCU sets per CU, where the whole grid is about one round of
-// resident waves (with inputs from HBM: 2048 x 16384 35.2 -> 32.3 us,
-// 4096 x 8192 34.2 -> 31.2 us; neutral at 8192^2 (64 sets per CU), 5 % slower
-// at 16384^2; profiles/r02/kbench2_wide_hbm_r02.log, kbench2_wide_r02.log),
-// the product's 512 otherwise.
-constexpr uint32_t kBigWgSetsPerCU = 32;
+// uint8 -> fp32 tile kernels (the headline):
+//  - frames of at most kBigWgSetsPerCU sets per CU, where the whole grid is
+//    about one round of resident waves: 1024-thread workgroups, no cap (4096^2:
+//    15.8 us against 17.9-18.8 capped; round 2: 2048 x 16384 35.2 -> 32.3 us);
+//  - larger frames: one-wave workgroups, at most kF32CapWavesPerCU resident
+//    per CU (12 up to 32 sets per CU).  8192^2: 58.6-58.7 us at 9-10 waves/CU
+//    against 61.8-62.1 for the uncapped 512-thread kernel and 62.5 for the
+//    uncapped one-wave kernel; 16384^2: 218-219 against 238; 2048 x 16384:
+//    33.7 against 35.0 (profiles/r03/m/kb3_occsz_*.log).  With the cap the
+//    packed-fp32 transform (kVarPacked) gains another 1-2 % (8192^2: 57.6 at
+//    10 waves/CU against 58.7 for the scalar form).
+constexpr uint32_t kBigWgSetsPerCU = 16;
+constexpr uint32_t kMidCapSetsPerCU = 32;
+constexpr uint32_t kF32CapWavesPerCUMid = 12;
+constexpr unsigned kOneWaveWg = 1u << 12;
 
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                         const QParams& q, float shift, hipStream_t s) {
     if constexpr (std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float>) {
-        if ((g.ntiles + 63u) / 64u <= kBigWgSetsPerCU * device_cus())
+        const uint32_t sets_per_cu = ((g.ntiles + 63u) / 64u + device_cus() - 1u) / device_cus();
+        if (sets_per_cu <= kBigWgSetsPerCU)
             return fdct_go<(kV & ~(3u << 12)) | (3u << 12), TIn, TOut, kQuant, kBuiltinT, kWriteback>(
                 img, out, shifted, g, t_dev, q, shift, s);
+        return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg | kVarPacked, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+            img, out, shifted, g, t_dev, q, shift, s,
+            sets_per_cu <= kMidCapSetsPerCU ? kF32CapWavesPerCUMid : kF32CapWavesPerCU);
     }
     return fdct_go<kV, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
 }
@@ -111,9 +156,36 @@ hipError_t fdct_octet_go(const TIn* img, TOut* out, float* shifted, const TileGr
     return hipGetLastError();
 }
 
+// fp32 -> fp32 duo inverse and row-first kernels: the headline's residency cap
+// once the grid holds at least kDuoCapWavesPerCU of their waves (32 tiles each)
+// per CU: one-wave workgroups, at most kDuoCapWaves resident per CU.  8192^2
+// inverse 86.0 against 89.0-89.4 us (profiles/r03/m/kb3_invb_8192.log); driver
+// bench: idct_all_blocks_cuda 89.7 -> 86.8, cublasDCTv2 pair 139.3 / 139.5 ->
+// 137.3 / 132.4.
+constexpr uint32_t kDuoCapWavesPerCU = 64;
+constexpr uint32_t kDuoCapWaves = 10;
+
+// (kernel, block variant, dynamic LDS) for a duo launch of the grid g
+template <unsigned kV>
+struct DuoShape {
+    static constexpr unsigned kCapped = (kV & ~(3u << 12)) | kOneWaveWg;
+    static bool capped(const TileGrid& g) {
+        const uint32_t waves = (g.ntiles + kDuoTiles - 1u) / kDuoTiles;
+        return waves >= kDuoCapWavesPerCU * device_cus();
+    }
+};
+template <typename K>
+size_t duo_cap_lds(K kern) {
+    static const size_t st = static_lds_of(kern);
+    return residency_cap_lds(st, kDuoCapWaves);
+}
+
 template <unsigned kV, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_duo_go(const float* img, float* out, float* shifted, const TileGrid& g, const float* t_dev,
                        const QParams& q, float shift, hipStream_t s) {
+    // uncapped: the quantising fp32 forward (caller's T, full chains, IEEE
+    // division) is VALU-heavy, and the cap made it slower in the driver's bench
+    // (91.6 -> 101.8 us, drop-in with write-back 135.6 -> 135.1)
     hipLaunchKernelGGL((fdct_duo_kernel<kQuant, kBuiltinT, kWriteback, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>),
                        0, s, img, out, shifted, g, t_dev, q, shift);
     return hipGetLastError();
@@ -122,6 +194,15 @@ hipError_t fdct_duo_go(const float* img, float* out, float* shifted, const TileG
 template <unsigned kV, bool kDequant, bool kBuiltinT, typename TOut>
 hipError_t idct_duo_go(const float* coef, TOut* out, float* dq_out, const TileGrid& g, const float* t_dev,
                        const Mat64& q, float shift, hipStream_t s) {
+    if constexpr (std::is_same_v<TOut, float>) {
+        if (DuoShape<kV>::capped(g)) {
+            constexpr unsigned kC = DuoShape<kV>::kCapped;
+            auto* kern = idct_duo_kernel<kDequant, kBuiltinT, kC, TOut>;
+            hipLaunchKernelGGL(kern, duo_grid(g, kBlock<kC>), dim3(kBlock<kC>), duo_cap_lds(kern), s, coef, out, dq_out,
+                               g, t_dev, q, shift);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((idct_duo_kernel<kDequant, kBuiltinT, kV, TOut>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>), 0,
                        s, coef, out, dq_out, g, t_dev, q, shift);
     return hipGetLastError();
@@ -130,6 +211,13 @@ hipError_t idct_duo_go(const float* coef, TOut* out, float* dq_out, const TileGr
 template <unsigned kV, bool kInv, bool kQ, bool kBuiltinT, bool kWb>
 hipError_t rowfirst_duo_go(const float* src, float* out, float* wb, const TileGrid& g, const float* t_dev,
                            const Mat64& q, float shift, hipStream_t s) {
+    if (DuoShape<kV>::capped(g)) {
+        constexpr unsigned kC = DuoShape<kV>::kCapped;
+        auto* kern = rowfirst_duo_kernel<kInv, kQ, kBuiltinT, kWb, kC>;
+        hipLaunchKernelGGL(kern, duo_grid(g, kBlock<kC>), dim3(kBlock<kC>), duo_cap_lds(kern), s, src, out, wb, g,
+                           t_dev, q, shift);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((rowfirst_duo_kernel<kInv, kQ, kBuiltinT, kWb, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>),
                        0, s, src, out, wb, g, t_dev, q, shift);
     return hipGetLastError();
@@ -274,6 +362,21 @@ hipError_t launch_idct_impl(const TIn* coef, TOut* out, float* dq_out, const Til
 // not a multiple of 512 px; grid (workgroups per frame, frames).
 template <unsigned kV, typename TOut>
 hipError_t fdct_frames_go(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, hipStream_t s) {
+    if constexpr (std::is_same_v<TOut, float>) {
+        // the headline's residency cap when the whole list is a large grid
+        const uint64_t sets = static_cast<uint64_t>((g.ntiles + 63u) / 64u) * static_cast<uint64_t>(n);
+        const uint64_t per_cu = (sets + device_cus() - 1u) / device_cus();
+        if (per_cu > kBigWgSetsPerCU) {
+            constexpr unsigned kC = (kV & ~(3u << 12)) | kOneWaveWg | kVarPacked;
+            auto* kern = fdct_frames_kernel<TOut, kC>;
+            static const size_t st = static_lds_of(kern);
+            const size_t dyn =
+                residency_cap_lds(st, per_cu <= kMidCapSetsPerCU ? kF32CapWavesPerCUMid : kF32CapWavesPerCU);
+            const dim3 grid(grid_for(g, false, 0, kBlock<kC>).x, static_cast<uint32_t>(n));
+            hipLaunchKernelGGL(kern, grid, dim3(kBlock<kC>), dyn, s, ft, g, q);
+            return hipGetLastError();
+        }
+    }
     const dim3 grid(grid_for(g, false, 0, kBlock<kV>).x, static_cast<uint32_t>(n));
     hipLaunchKernelGGL((fdct_frames_kernel<TOut, kV>), grid, dim3(kBlock<kV>), 0, s, ft, g, q);
     return hipGetLastError();

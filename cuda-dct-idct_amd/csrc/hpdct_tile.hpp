@@ -117,6 +117,55 @@ __device__ __forceinline__ void fdct_tile(const TS& T, float (&x)[8][8], Emit&& 
     });
 }
 
+// Packed-fp32 forward (v_pk_fma_f32: two IEEE fmas per instruction, each half
+// rounded exactly like the scalar v_fma_f32; round 3), built-in T, finite
+// inputs only (uint8 pixels).  Same chains as fdct_tile: pass 1 pairs the
+// columns (x, x+1) of one P row; pass 2 pairs output columns whose zero
+// patterns in T coincide, (0,2) (4,6) (1,5) (3,7), so a term that is zero in
+// one half only adds fma(0, P, s) = s exactly (P finite, s never -0).
+// emit2(v, c2): c2[k] = {C[v][pair_u(k, 0)], C[v][pair_u(k, 1)]}.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// (a function, not a table: indexing a namespace-scope table here made hipcc
+// keep the quotient operands in scratch memory)
+constexpr int pair_u(int k, int h) {
+    return k == 0 ? (h ? 2 : 0) : k == 1 ? (h ? 6 : 4) : k == 2 ? (h ? 5 : 1) : (h ? 7 : 3);
+}
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <typename Emit2>
+__device__ __forceinline__ void fdct_tile_pk(const f32x2 (&x2)[8][4], Emit2&& emit2) {
+    f32x2 p2[8][4];
+    // P = T . X, two columns per instruction (main_newAppr.cu:193-197)
+    unroll<8>([&](auto v) {
+        unroll<4>([&](auto cp) {
+            f32x2 s = {0.0f, 0.0f};
+            unroll<8>([&](auto i) {
+                constexpr float c = kBuiltinT.v[v * 8 + i];
+                if constexpr (c != 0.0f) s = fma2(f32x2{c, c}, x2[i][cp], s);
+            });
+            p2[v][cp] = s;
+        });
+    });
+    // C = P . T^T, two output columns per instruction (main_newAppr.cu:206-209)
+    unroll<8>([&](auto v) {
+        f32x2 c2[4];
+        unroll<4>([&](auto k) {
+            constexpr int u0 = pair_u(k, 0), u1 = pair_u(k, 1);
+            f32x2 s = {0.0f, 0.0f};
+            unroll<8>([&](auto i) {
+                constexpr float a = kBuiltinT.v[u0 * 8 + i], b = kBuiltinT.v[u1 * 8 + i];
+                if constexpr (a != 0.0f || b != 0.0f) {
+                    const float pv = p2[v][i / 2][i % 2];
+                    s = fma2(f32x2{a, b}, f32x2{pv, pv}, s);
+                }
+            });
+            c2[k] = s;
+        });
+        emit2(v, c2);
+    });
+}
+
 // cublasDCTv2 pass order (main_cublass_2.cu:228-235): R = X.T^T (row pass,
 // temp1) first, then C = T.R, each a sequential FMA chain over the 8
 // non-trivial terms of the block-diagonal GEMM's k range.
