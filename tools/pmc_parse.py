@@ -24,7 +24,7 @@ CALIB_BYTES = 256 << 20
 
 
 def per_dispatch(dirpath, counter):
-    """{kernel_name: [value per dispatch]} from a rocprofv3 counter csv."""
+    """{(kernel_name, grid_size): [value per dispatch]} from a rocprofv3 counter csv."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
     files += glob.glob(dirpath + ".counter_collection.csv")  # the flattened copies under profiles/
     out = {}
@@ -32,13 +32,16 @@ def per_dispatch(dirpath, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+            out.setdefault((r["Kernel_Name"], int(r.get("Grid_Size") or 0)), []).append(float(r["Counter_Value"]))
     return out
 
 
-def pick(d, needle, exclude=()):
-    for k, v in d.items():
-        if needle in k and not any(e in k for e in exclude):
+def pick(d, needle, exclude=(), grid=None):
+    """dispatch values of the first kernel whose name holds needle (and none of
+    exclude), at the given grid size (threads) when one is given: since round 3
+    the headline kernel also runs the C2 batch (same name, a smaller grid)"""
+    for (name, g), v in d.items():
+        if needle in name and not any(e in name for e in exclude) and (grid is None or g == grid):
             return v
     raise KeyError(needle)
 
@@ -81,9 +84,11 @@ def main():
     n = 8192
     kernels = {}
     for key, (needle, excl, rw, ww, rb, wb) in KERNELS.items():
+        # launch grid at 8192^2: one lane per tile for the tile kernels, two for duo
+        grid = n * n // 32 if "duo" in needle else n * n // 64
         try:
-            kf = statistics.median(pick(fetch, needle, excl))
-            kw = statistics.median(pick(write, needle, excl))
+            kf = statistics.median(pick(fetch, needle, excl, grid))
+            kw = statistics.median(pick(write, needle, excl, grid))
         except KeyError:
             continue
         read_b = kf * 1024 * scale[rw]
