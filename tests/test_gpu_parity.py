@@ -494,6 +494,29 @@ def test_video_widths_large_frames(hp, oracle, dev, h, w):
     assert sums["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
 
 
+@pytest.mark.parametrize("h,w", [(4104, 8200), (3000, 8008), (2048, 16384)])
+@pytest.mark.parametrize("qtab", ["jpeg", "fractional"])
+def test_capped_packed_forward_large_frames(hp, oracle, dev, h, w, qtab):
+    """u8 -> fp32 frames of more than 16 sets per CU take the one-wave,
+    residency-capped, packed-fp32 kernel (hpdct_launch.hpp fdct_tile_go):
+    cap 10 above 32 sets per CU (4104 x 8200), cap 12 up to 32 (3000 x 8008,
+    2048 x 16384).  Ragged widths (tiles_x not a multiple of 64: sets straddle
+    tile rows) and a ragged last set; the JPEG table (3-op quotient per half)
+    and a fractional table (IEEE division per half).  Bit-exact vs the oracle."""
+    img = oracle.hash_u8(h * w, seed=h + w).reshape(h, w)
+    Q = None
+    if qtab == "fractional":
+        Q = np.random.default_rng(5).uniform(1.0, 50.0, (8, 8)).astype(np.float32)
+        hp.set_quant_table(Q)
+    try:
+        got = to_host(hp.forward(to_dev(img, dev)))
+    finally:
+        if Q is not None:
+            hp.set_quant_table(None)
+    ref = oracle.fdct(img) if Q is None else oracle.fdct(img, Q=Q)
+    assert bits_equal(got, ref), mismatches(got, ref)
+
+
 # --------------------------------------------------------------------- full-size configs
 def test_c2_1024_bitexact(hp, oracle, dev, golden):
     img = oracle.rand_u8(1024 * 1024).reshape(1024, 1024)
