@@ -238,8 +238,9 @@ hpdct_status hpdct_forward(const void* d_image, hpdct_dtype in_type, void* d_coe
     if (out_type == HPDCT_I8 && !qs.int8_ok)
         return fail(HPDCT_ERROR_RANGE, "current quant table can produce |q| > 127: use fp32 output");
     const QParams& qp = qs.qp;
-    // |C| <= 8*255 for uint8 input with the built-in T, well inside the verified |C| <= 4096
-    const bool fastdiv = quant && in_type == HPDCT_U8 && d_transform == nullptr && qs.fastdiv_ok;
+    // |C| <= 8*255 for uint8 input with the built-in T, well inside the verified |C| <= 4096;
+    // fp32 input (any T) takes it row by row behind a range test (kVarFastDivChecked, duo kernels)
+    const bool fastdiv = quant && qs.fastdiv_ok && ((in_type == HPDCT_U8 && d_transform == nullptr) || in_type == HPDCT_F32);
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool bt = d_transform == nullptr;

@@ -143,7 +143,14 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
             unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(row[i], s); });
             dst[u] = s;
         });
-        if constexpr (kQuant) {  // row 4h+k of Q: two kernel-argument values, one select
+        if constexpr (kQuant && (kVar & kVarFastDivChecked) != 0) {  // row 4h+k of Q and 1/Q
+            float qv[8], rv[8];
+            unroll<8>([&](auto u) {
+                qv[u] = h ? qp.q.v[(4 + k) * 8 + u] : qp.q.v[k * 8 + u];
+                rv[u] = h ? qp.r.v[(4 + k) * 8 + u] : qp.r.v[k * 8 + u];
+            });
+            quantise_row_checked(dst, qv, rv);
+        } else if constexpr (kQuant) {  // row 4h+k of Q: two kernel-argument values, one select
             unroll<8>([&](auto u) {
                 const float qv = h ? qp.q.v[(4 + k) * 8 + u] : qp.q.v[k * 8 + u];
                 dst[u] = quantise<kVar>(dst[u], qv, 0.0f);

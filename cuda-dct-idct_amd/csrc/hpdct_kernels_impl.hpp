@@ -37,6 +37,10 @@ enum : unsigned {
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
+    kVarFastDivChecked = 1u << 23,  // fp32 input (any T), integer table in 1..255: the 3-op quotient for an
+                                    // output row when every lane's 8 values have |C| <= 4096 (wave-uniform
+                                    // test, NaN/inf fail it), IEEE division otherwise: exact either way
+                                    // (verify_fastdiv covers every |C| <= 4096)
     kVarPacked = 1u << 19,    // uint8 -> fp32 quantised, built-in T: packed-fp32 transform and quotient
                               // (fdct_tile_pk; 844 instead of 1,308 VALU instructions per set)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
@@ -169,6 +173,22 @@ __device__ __forceinline__ float quantise(float c, float q, float r) {
         d = c / q;  // IEEE (hipcc default: correctly rounded fp32 division)
     }
     return round_half_away(d);
+}
+
+// divide_matrices for one output row of 8 values per lane, kVarFastDivChecked:
+// the verified 3-op quotient when the whole wave's row is within |C| <= 4096,
+// IEEE division otherwise (a wave-uniform branch).
+__device__ __forceinline__ void quantise_row_checked(float (&d)[8], const float (&q)[8], const float (&r)[8]) {
+    float m = 0.0f;
+    unroll<8>([&](auto u) { m = __builtin_fmaxf(m, __builtin_fabsf(d[u])); });
+    // !(m <= 4096) also catches NaN (fmax drops a NaN operand, so test every value)
+    bool bad = !(m <= 4096.0f);
+    unroll<8>([&](auto u) { bad = bad || (d[u] != d[u]); });
+    if (__builtin_amdgcn_ballot_w64(bad) == 0) {
+        unroll<8>([&](auto u) { d[u] = quantise<kVarFastDiv>(d[u], q[u], r[u]); });
+    } else {
+        unroll<8>([&](auto u) { d[u] = quantise<0u>(d[u], q[u], r[u]); });
+    }
 }
 
 // Tile-set geometry: lane's tile and the element offset of its top-left pixel.

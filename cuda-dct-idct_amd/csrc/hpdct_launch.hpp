@@ -242,8 +242,15 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
     constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
     const Mapping map = pick_mapping(g, kF32);
     if constexpr (kF32) {
-        if (map == Mapping::kDuo)
+        if (map == Mapping::kDuo) {
+            if constexpr (kQuant) {  // integer table: the range-checked 3-op quotient
+                if (fastdiv)
+                    return fdct_duo_go<kDuoVar | kVarFastDivChecked, kQuant, kBuiltinT, kWriteback>(img, out, shifted,
+                                                                                                    g, t_dev, q,
+                                                                                                    shift, s);
+            }
             return fdct_duo_go<kDuoVar, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
+        }
     }
     if (map == Mapping::kOctet) {
         if constexpr (kFastDivOk) {
