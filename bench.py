@@ -145,6 +145,13 @@ def main():
     # one process per GPU: LOCAL_RANK is the device (modulo the visible devices,
     # so a gloo rehearsal can put several ranks on one GPU)
     ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > 1 and world > ndev:
+        # RCCL needs one GPU per rank (it refuses two ranks on one device only
+        # after every rank is already inside communicator setup): say so now,
+        # before any RCCL or HIP call
+        print(f"--backend nccl needs one GPU per rank: WORLD_SIZE={world} ranks but {ndev} visible device(s); "
+              "use --backend gloo to rehearse several ranks on fewer GPUs", file=sys.stderr)
+        return 2
     local_dev = local % ndev if ndev else local
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -291,6 +298,9 @@ def main():
         "vs_baseline_ref": "T4 14.70 ms (README.md:55) = 4.57 Gpixel/s, fp32-in 3-kernel path",
         "parity_spot_check": parity,
         "host_wall_s": round(wall, 4),
+        # which sources built the library that was timed (src_digest.py): the
+        # digest stamped at build time vs the digest of this tree's sources
+        "provenance": hpdct.provenance(),
     }
 
     # ------------------------------------------------------------ sustained headline
@@ -309,7 +319,9 @@ def main():
         result["extras"] = extras
         c4 = extras.get("c4", {})
         # the north_star row-shard figures (C4, 16384^2 over the ranks), top level
-        for key in ("compute_speedup_vs_1gpu", "gather_ms", "gather_int8_ms", "sharded_equals_unsharded"):
+        for key in ("compute_speedup_vs_1gpu", "predicted_compute_speedup_2", "predicted_compute_speedup_4",
+                    "predicted_compute_speedup_8", "one_gpu_full_frame_ms", "gather_ms", "gather_int8_ms",
+                    "decode_int8_ms", "end_to_end_ms", "end_to_end_int8_ms", "sharded_equals_unsharded"):
             if key in c4:
                 result["c4_" + key] = c4[key]
         if "compute_ms_max_rank" in c4:
@@ -534,8 +546,9 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         del fl_in, fl_out, calls
         torch.cuda.empty_cache()
         if not args.no_c4c5:
+            use_pg = world > 1 or "WORLD_SIZE" in os.environ  # as main()
             extras["c4"] = _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks,
-                               timed_loop)
+                               timed_loop, use_pg)
             extras["c5"] = _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks)
 
 
@@ -642,97 +655,179 @@ def _steady_ms(torch, calls, steps, stream):
     return a.elapsed_time(b) / steps
 
 
-def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop):
+def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop, use_pg):
     """C4: one 16384^2 frame row-sharded over the ranks (device-generated by
-    the stateless hash so no H2D), forward kernel per slab, then the gather
-    of the coefficient slabs to rank 0, timed separately.  With the nccl
-    backend the gather is the native C-ABI (include/hpdct_dist.h:
-    hpdct_gather_rows, ncclSend/ncclRecv over xGMI) on a communicator of its
-    own, at every world size including 1 (then a device-to-device copy of the
-    root's own slab); the gloo rehearsal (several ranks on one GPU, which RCCL
-    cannot serve) keeps torch.distributed's gather."""
+    the stateless hash so no H2D), the forward kernel per slab, the gather of
+    the coefficient slabs to rank 0.  Reported:
+
+      compute_ms_max_rank        this run's slab kernel, max over ranks;
+      one_gpu_full_frame_ms      the whole frame on one GPU (rank 0);
+      predicted_compute_speedup_{2,4,8}
+                                 full frame / the rank-0 slab of a k-way split,
+                                 both timed on THIS GPU at every world size
+                                 (world 1 included): the compute-phase node
+                                 speedup k GPUs would give (north_star >= 6x
+                                 at 8), measured without k GPUs;
+      gather_ms / gather_int8_ms the gather alone (the root computes its own
+                                 slab in place in the frame, so only peer bytes
+                                 move: 0 at world 1);
+      decode_int8_ms             the root's int8 -> fp32 decode (HIP kernel);
+      end_to_end_ms / end_to_end_int8_ms
+                                 slab forward + gather (+ decode) between two
+                                 barriers, max over ranks: what a caller that
+                                 needs the whole fp32 frame on one GPU waits.
+
+    With the nccl backend the gather is the native C-ABI
+    (include/hpdct_dist.h: hpdct_gather_rows, ncclSend/ncclRecv over xGMI) on a
+    communicator of its own; the gloo rehearsal (several ranks on one GPU,
+    which RCCL cannot serve) uses torch.distributed's gather; a single process
+    without a process group has nothing to gather."""
     from hpdct_dist import gather_slabs
     n = args.c4_size
     r0, rows = hpdct.shard_rows_native(n, world, rank)
-    # identical slab buffer sets, rotated: their inputs total >= 4x the
-    # Infinity Cache (at 8 ranks a slab reads 32 MiB: 32 sets)
+    reps = EXTRA_STEPS
+
+    def slab_ms(first, nrows):
+        """steady-state time of the forward over an nrows x n slab (rows from
+        `first` of the frame), inputs rotated past the Infinity Cache"""
+        nsl = sets_for(nrows * n)
+        xs = [torch.empty((nrows, n), dtype=torch.uint8, device=dev) for _ in range(nsl)]
+        for t in xs:
+            hpdct.fill_hash_u8(t, seed=42, first_index=first * n)
+        ys = [torch.empty((nrows, n), dtype=torch.float32, device=dev) for _ in range(nsl)]
+        calls = [hpdct.bind("fwd", xs[i], ys[i], stream=stream) for i in range(nsl)]
+        ms = _steady_ms(torch, calls, reps, stream)
+        del xs, ys, calls
+        torch.cuda.empty_cache()
+        return ms, nsl
+
+    # this run's slab, timed on every rank together
     nsl = sets_for(rows * n)
     xs = [torch.empty((rows, n), dtype=torch.uint8, device=dev) for _ in range(nsl)]
     for t in xs:
         hpdct.fill_hash_u8(t, seed=42, first_index=r0 * n)
     ys = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(nsl)]
-    x, y = xs[0], ys[0]
     calls = [hpdct.bind("fwd", xs[i], ys[i], stream=stream) for i in range(nsl)]
-    reps = EXTRA_STEPS
     rms, _, _ = timed_loop(calls, reps, 4)
     compute_ms = max_over_ranks(rms / reps)
+    x = xs[0]
+    del xs[1:], ys, calls
+    torch.cuda.empty_cache()
     out = {"frame": [n, n], "rows_per_rank": rows, "slab_sets": nsl, "compute_ms_max_rank": round(compute_ms, 4),
            "compute_gpx_s": round(n * n / (compute_ms * 1e-3) / 1e9, 2),
            "compute_hbm_frac_max_rank": round(5 * rows * n / (compute_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    # the full frame and the k-way rank-0 slabs on this GPU (rank 0; the others wait)
+    if rank == 0:
+        full_ms, _ = slab_ms(0, n)
+        out["one_gpu_full_frame_ms"] = round(full_ms, 4)
+        pred = {}
+        for k in (2, 4, 8):
+            f0, kr = hpdct.shard_rows_native(n, k, 0)
+            ms, _ = slab_ms(f0, kr)
+            pred[str(k)] = {"rows": kr, "slab_ms": round(ms, 4), "speedup": round(full_ms / ms, 2)}
+        out["predicted_compute"] = pred
+        for k in (2, 4, 8):
+            out[f"predicted_compute_speedup_{k}"] = pred[str(k)]["speedup"]
+        if world > 1:
+            out["compute_speedup_vs_1gpu"] = round(full_ms / compute_ms, 2)
+    barrier()
+
     comm = None
-    if args.backend == "nccl":
+    if args.backend == "nccl" and (use_pg or world == 1):
         if world == 1:
             comm = hpdct.Comm.init_all([dev.index])[0]
         else:
             uid = [hpdct.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             comm = hpdct.Comm.init_rank(world, uid[0], rank, dev.index)
-        out["gather_path"] = "native RCCL: hpdct_gather_rows (ncclSend/ncclRecv group), libhpdct_dist.so"
-        hpdct.forward_slab(comm, x, y, n, n, stream=stream)  # y = this rank's slab (set 0), via the C-ABI
-    else:
+        out["gather_path"] = ("native RCCL: hpdct_gather_rows (ncclSend/ncclRecv group), libhpdct_dist.so; the "
+                              "root's slab computed in place in the frame")
+    elif use_pg:
         out["gather_path"] = "torch.distributed gather (gloo rehearsal, staged through host memory)"
-        hpdct.forward(x, y)
+    else:
+        out["gather_path"] = "none (one process, no process group: the slab is the frame)"
 
-    def gather(slab):
-        if comm is None:
-            return gather_slabs(slab, n, n, root=0)
-        frame = torch.empty((n, n), dtype=slab.dtype, device=dev) if rank == 0 else None
-        hpdct.gather_rows(comm, slab, frame, n, n, root=0, stream=stream)
-        return frame
+    # root: the frame buffers, its own slab written in place; others: slab buffers
+    frame = torch.empty((n, n), dtype=torch.float32, device=dev) if rank == 0 else None
+    frame8 = torch.empty((n, n), dtype=torch.int8, device=dev) if rank == 0 else None
+    in_place = comm is not None or not use_pg
+    if rank == 0 and in_place:
+        y, y8 = frame[r0:r0 + rows], frame8[r0:r0 + rows]
+    else:
+        y = torch.empty((rows, n), dtype=torch.float32, device=dev)
+        y8 = torch.empty((rows, n), dtype=torch.int8, device=dev)
 
-    def timed_gather(slab):
-        ms, frame = [], None
-        for _ in range(3):
-            frame = None
+    def forward(dst):
+        if comm is not None:
+            hpdct.forward_slab(comm, x, dst, n, n, stream=stream)
+        else:
+            hpdct.forward(x, dst)
+
+    def gather(slab, full):
+        if comm is not None:
+            hpdct.gather_rows(comm, slab, full, n, n, root=0, stream=stream)
+            return full
+        if not use_pg:
+            return full  # computed in place: the slab is the frame
+        got = gather_slabs(slab, n, n, root=0)
+        if rank == 0:
+            full.copy_(got)
+        return full
+
+    def timed(fn, tries=3):
+        best = None
+        for _ in range(tries):
             barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            frame = gather(slab)
+            fn()
             torch.cuda.synchronize()
-            ms.append((time.perf_counter() - t0) * 1e3)
-        return round(max_over_ranks(min(ms)), 3), frame
+            ms = (time.perf_counter() - t0) * 1e3
+            best = ms if best is None else min(best, ms)
+        return round(max_over_ranks(best), 4)
 
-    out["gather_ms"], full = timed_gather(y)
-    out["gather_bytes_to_root"] = (n * n - rows * n) * 4
-    # int8 wire format (|q| <= 98): forward to int8, gather 1 B/coef, decode on the root
-    y8 = torch.empty((rows, n), dtype=torch.int8, device=dev)
-    hpdct.forward(x, y8)
-    out["gather_int8_ms"], full8 = timed_gather(y8)
+    peer_rows = n - rows
+    forward(y)
+    out["gather_ms"] = timed(lambda: gather(y, frame))
+    out["gather_bytes_to_root"] = peer_rows * n * 4 if rank == 0 else None
+    forward(y8)
+    out["gather_int8_ms"] = timed(lambda: gather(y8, frame8))
+    out["gather_int8_bytes_to_root"] = peer_rows * n if rank == 0 else None
+    full_dec = torch.empty((n, n), dtype=torch.float32, device=dev) if rank == 0 else None
     if rank == 0:
-        out["int8_wire_equals_fp32"] = bool(torch.equal(full8.float(), full))
-    del y8, full8
+        dec_ms = _steady_ms(torch, [lambda: hpdct.decode_i8_f32(frame8, full_dec, stream=stream)], reps // 4,
+                            stream)
+        out["decode_int8_ms"] = round(dec_ms, 4)
+        out["decode_int8_hbm_frac"] = round(5 * n * n / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+
+    def e2e_f32():
+        forward(y)
+        gather(y, frame)
+
+    def e2e_i8():
+        forward(y8)
+        gather(y8, frame8)
+        if rank == 0:
+            hpdct.decode_i8_f32(frame8, full_dec, stream=stream)
+
+    out["end_to_end_ms"] = timed(e2e_f32)
+    out["end_to_end_int8_ms"] = timed(e2e_i8)
+    out["end_to_end_note"] = ("slab forward + gather (+ int8 decode on the root) between barriers, host clock, best "
+                              "of 3, max over ranks; compare one_gpu_full_frame_ms (the whole frame on one GPU)")
     if rank == 0:
         # sharded + gathered == the whole frame computed on one GPU
         xf = torch.empty((n, n), dtype=torch.uint8, device=dev)
         hpdct.fill_hash_u8(xf, seed=42, first_index=0)
         ref = hpdct.forward(xf)
-        out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
-        del full
-        if world > 1:
-            # the same full frame on this one GPU: the compute-phase node speedup
-            # (BASELINE.md C4 target >= 6x at 8 GPUs); sets rotated as above
-            xfs = [xf] + [xf.clone() for _ in range(sets_for(n * n) - 1)]
-            refs = [ref] + [torch.empty_like(ref) for _ in range(len(xfs) - 1)]
-            fcalls = [hpdct.bind("fwd", a, b, stream=stream) for a, b in zip(xfs, refs)]
-            one_gpu_ms = _steady_ms(torch, fcalls, reps, stream)
-            out["one_gpu_full_frame_ms"] = round(one_gpu_ms, 4)
-            out["compute_speedup_vs_1gpu"] = round(one_gpu_ms / compute_ms, 2)
-            del xfs, refs
+        torch.cuda.synchronize()
+        out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), frame.view(torch.int32)))
+        out["int8_wire_equals_fp32"] = bool(torch.equal(full_dec, ref))  # by value: a -0.0 decodes as +0.0
         del xf, ref
     barrier()
     if comm is not None:
         comm.destroy()
-    del x, y, xs, ys
+    del x, y, y8, frame, frame8, full_dec
     torch.cuda.empty_cache()
     return out
 

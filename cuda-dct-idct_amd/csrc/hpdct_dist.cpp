@@ -4,23 +4,43 @@
 // ncclSend / ncclRecv pairs inside one group (rccl.h:700,722), which also
 // covers slabs that differ by a tile row (ncclGather, rccl.h:745, needs equal
 // counts).  Bytes travel as ncclUint8: the element type does not matter to a
-// gather.
+// gather.  Before the first gather of a geometry, the ranks check that they
+// agree on it (hpdct_dist_geometry.hpp): a disagreement is an error on every
+// rank instead of sends and receives of different sizes that never complete.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 
 #include "hpdct.h"
 #include "hpdct_dist.h"
+#include "hpdct_dist_geometry.hpp"
 #include "hpdct_kernels.h"
 
 static_assert(HPDCT_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "hpdct_unique_id size");
 
+namespace {
+// Communicators of one hpdct_comm_init_all call live in this process: each
+// round of gathers (one per communicator, normally inside one
+// hpdct_group_start/end) is compared on the host, no collective needed.
+struct Clique {
+    std::mutex m;
+    int reported = 0;  // gathers of the current round so far
+    hpdct::dist::Geometry g{};
+};
+thread_local int t_group_depth = 0;
+}  // namespace
+
 struct hpdct_comm_s {
     ncclComm_t nccl;
     int rank, size, device;
+    std::shared_ptr<Clique> clique;   // init_all communicators only
+    hpdct::dist::AgreedSet agreed;    // init_rank: geometries the ranks agreed on
+    int64_t* d_check = nullptr;       // init_rank: 64 B for the agreement all-reduce
 };
 
 namespace {
@@ -70,6 +90,54 @@ hpdct_status check_geometry(hpdct_comm comm, int64_t height, int64_t width) {
     return HPDCT_SUCCESS;
 }
 
+// The ranks agree on this gather's geometry (see the file comment).
+// (A one-rank per-process communicator runs the check too: it is once per
+// geometry, and it keeps the all-reduce path exercised on a one-GPU box.)
+hpdct_status check_agreement(hpdct_comm comm, const hpdct::dist::Geometry& g, hipStream_t s) {
+    if (comm->clique) {
+        Clique& c = *comm->clique;
+        std::lock_guard<std::mutex> lock(c.m);
+        if (c.reported == 0) c.g = g;  // the round's first gather sets the geometry
+        const bool same = c.g == g;
+        if (++c.reported == comm->size) c.reported = 0;  // round complete
+        if (same) return HPDCT_SUCCESS;
+        return fail(HPDCT_ERROR_INVALID_VALUE,
+                    "gathers of one round disagree on (height, width, type, root) across the communicators");
+    }
+    if (comm->agreed.contains(g)) return HPDCT_SUCCESS;
+    if (t_group_depth > 0)
+        return fail(HPDCT_ERROR_INVALID_VALUE,
+                    "the first gather of a new geometry on a per-process communicator must be outside "
+                    "hpdct_group_start/end (its agreement check synchronises the stream)");
+    if (!comm->d_check) {
+        void* p = nullptr;
+        if (hpdct_status st = hip_status(hipMalloc(&p, sizeof(int64_t) * hpdct::dist::kCheckWords), "hipMalloc"))
+            return st;
+        comm->d_check = static_cast<int64_t*>(p);
+    }
+    int64_t v[hpdct::dist::kCheckWords];
+    hpdct::dist::pack_for_max(g, v);
+    if (hpdct_status st = hip_status(hipMemcpyAsync(comm->d_check, v, sizeof(v), hipMemcpyHostToDevice, s),
+                                     "hipMemcpyAsync"))
+        return st;
+    if (hpdct_status st = nccl_status(ncclAllReduce(comm->d_check, comm->d_check, hpdct::dist::kCheckWords,
+                                                    ncclInt64, ncclMax, comm->nccl, s),
+                                      "ncclAllReduce (geometry check)"))
+        return st;
+    if (hpdct_status st = hip_status(hipMemcpyAsync(v, comm->d_check, sizeof(v), hipMemcpyDeviceToHost, s),
+                                     "hipMemcpyAsync"))
+        return st;
+    if (hpdct_status st = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return st;
+    if (!hpdct::dist::agree_after_max(v))
+        return fail(HPDCT_ERROR_INVALID_VALUE,
+                    "ranks disagree on the gather's (height, width, type, root): max (" + std::to_string(v[0]) +
+                        ", " + std::to_string(v[1]) + ", " + std::to_string(v[2]) + ", " + std::to_string(v[3]) +
+                        ") vs min (" + std::to_string(-v[4]) + ", " + std::to_string(-v[5]) + ", " +
+                        std::to_string(-v[6]) + ", " + std::to_string(-v[7]) + ")");
+    comm->agreed.add(g);
+    return HPDCT_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" {
@@ -93,8 +161,10 @@ hpdct_status hpdct_comm_init_all(hpdct_comm* comms, int ndev, const int* devices
         return st;
     }
     bool ok = true;
-    for (int i = 0; i < ndev; ++i) {
-        comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i]};
+    std::shared_ptr<Clique> clique(new (std::nothrow) Clique());
+    ok = clique != nullptr;
+    for (int i = 0; i < ndev && ok; ++i) {
+        comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i], clique, {}, nullptr};
         ok = ok && comms[i];
     }
     if (!ok) {  // all or nothing: no communicator survives a failed call
@@ -126,7 +196,7 @@ hpdct_status hpdct_comm_init_rank(hpdct_comm* comm, int nranks, const hpdct_uniq
     memcpy(u.internal, id->internal, sizeof(u.internal));
     ncclComm_t c;
     if (hpdct_status st = nccl_status(ncclCommInitRank(&c, nranks, u, rank), "ncclCommInitRank")) return st;
-    *comm = new (std::nothrow) hpdct_comm_s{c, rank, nranks, device};
+    *comm = new (std::nothrow) hpdct_comm_s{c, rank, nranks, device, nullptr, {}, nullptr};
     if (!*comm) {
         (void)ncclCommDestroy(c);
         return fail(HPDCT_ERROR_DEVICE, "out of host memory");
@@ -136,6 +206,10 @@ hpdct_status hpdct_comm_init_rank(hpdct_comm* comm, int nranks, const hpdct_uniq
 
 hpdct_status hpdct_comm_destroy(hpdct_comm comm) {
     if (!comm) return HPDCT_SUCCESS;
+    if (comm->d_check) {
+        DeviceScope ds(comm->device);
+        (void)hipFree(comm->d_check);
+    }
     const hpdct_status st = nccl_status(ncclCommDestroy(comm->nccl), "ncclCommDestroy");
     delete comm;
     return st;
@@ -145,8 +219,15 @@ int hpdct_comm_rank(hpdct_comm comm) { return comm ? comm->rank : -1; }
 int hpdct_comm_size(hpdct_comm comm) { return comm ? comm->size : -1; }
 int hpdct_comm_device(hpdct_comm comm) { return comm ? comm->device : -1; }
 
-hpdct_status hpdct_group_start(void) { return nccl_status(ncclGroupStart(), "ncclGroupStart"); }
-hpdct_status hpdct_group_end(void) { return nccl_status(ncclGroupEnd(), "ncclGroupEnd"); }
+hpdct_status hpdct_group_start(void) {
+    const hpdct_status st = nccl_status(ncclGroupStart(), "ncclGroupStart");
+    if (st == HPDCT_SUCCESS) ++t_group_depth;
+    return st;
+}
+hpdct_status hpdct_group_end(void) {
+    if (t_group_depth > 0) --t_group_depth;
+    return nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+}
 
 hpdct_status hpdct_forward_slab(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,
                                 int64_t height, int64_t width, void* stream) {
@@ -170,6 +251,10 @@ hpdct_status hpdct_gather_rows(hpdct_comm comm, const void* d_slab, void* d_fram
     hipStream_t s = static_cast<hipStream_t>(stream);
     DeviceScope ds(comm->device);
     if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    const hpdct::dist::Geometry geo{{height, width, static_cast<int64_t>(type), root}};
+    if (hpdct_status st = check_agreement(comm, geo, s)) return st;
+    // one rank whose slab already sits in the frame: nothing moves
+    if (comm->size == 1 && d_frame == d_slab) return HPDCT_SUCCESS;
     int64_t first, rows;
     if (comm->rank != root) {
         shard(height, comm->size, comm->rank, first, rows);

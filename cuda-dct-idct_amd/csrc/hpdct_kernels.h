@@ -75,6 +75,9 @@ hipError_t launch_fdct_frames(const FrameTable<TOut>& ft, int n, const TileGrid&
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 
+// int8 wire coefficients -> fp32 plane (hpdct_decode.hip)
+hipError_t launch_decode_i8_f32(const int8_t* in, float* out, uint64_t n, hipStream_t s);
+
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.
 int mapping_mode();
 

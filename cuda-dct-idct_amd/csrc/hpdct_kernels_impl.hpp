@@ -29,15 +29,16 @@ namespace hpdct {
 enum : unsigned {
     kVarFastDiv = 1u,  // quotient by  q0=c*r; e=fma(-q0,Q,c); q=fma(e,r,q0)  (r = RN(1/Q)).  Gives the same
                        // roundf() as IEEE c/Q for every |c| <= 4096 and every integer Q in 1..255
-                       // (exhaustive: tests/tools/verify_fastdiv.*); only enabled for such tables and
-                       // uint8 input with the built-in T (|C| <= 1024).
+                       // (exhaustive: tests/tools/verify_fastdiv.*); enabled unconditionally only for such
+                       // tables with uint8 input and the built-in T (|C| <= 1024); fp32 input with such a
+                       // table takes it per output row under kVarFastDivChecked.
     kVarLdsStore = 8u, // fp32 rows re-staged through LDS so every store instruction writes 1 KiB contiguous
     kVarNT = 16u,      // non-temporal (streaming) stores for the output planes
     // bits 12..13: workgroup size: 0 -> 256 threads, 1 -> 64, 2 -> 512, 3 -> 1024
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
                               // (in-place multiply_matrices of main_cublass_2.cu:285)
-    kVarFastDivChecked = 1u << 23,  // fp32 input (any T), integer table in 1..255: the 3-op quotient for an
+    kVarFastDivChecked = 1u << 26,  // fp32 input (any T), integer table in 1..255: the 3-op quotient for an
                                     // output row when every lane's 8 values have |C| <= 4096 (wave-uniform
                                     // test, NaN/inf fail it), IEEE division otherwise: exact either way
                                     // (verify_fastdiv covers every |C| <= 4096)
@@ -50,6 +51,9 @@ enum : unsigned {
                               // 32 B per lane; launched only for such widths (the branch costs the
                               // power-of-two frames ~3 %, profiles/r01/ab_straddle.log)
 };
+// Bits only the product kernels give a meaning to: the tools' A/B variant
+// bits must stay clear of them (static_assert in tools/kbench_variants.hpp).
+constexpr unsigned kProductOnlyVarBits = kVarFastDivChecked;
 template <unsigned kVar>
 constexpr uint32_t kBlock = ((kVar >> 12) & 3u) == 1u   ? 64u
                             : ((kVar >> 12) & 3u) == 2u ? 512u

@@ -42,7 +42,7 @@ STATUS = {
 
 # every symbol include/hpdct.h and include/hpdct_compat.h declare
 C_SYMBOLS = [
-    "hpdct_version", "hpdct_status_string", "hpdct_last_error_string",
+    "hpdct_version", "hpdct_build_info", "hpdct_status_string", "hpdct_last_error_string",
     "hpdct_default_quant_table", "hpdct_default_transform",
     "hpdct_set_quant_table", "hpdct_get_quant_table",
     "hpdct_forward", "hpdct_inverse",
@@ -50,7 +50,7 @@ C_SYMBOLS = [
     "hpdct_fill_hash_u8", "hpdct_fill_rand_u8", "hpdct_u8_to_f32", "hpdct_f32_to_u8",
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
     "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate", "hpdct_forward_frames",
-    "hpdct_stream_create", "hpdct_stream_run", "hpdct_stream_destroy",
+    "hpdct_stream_create", "hpdct_stream_run", "hpdct_stream_destroy", "hpdct_decode_i8_f32",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -100,6 +100,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         raise HpdctLibraryError(f"cannot load {p}: {e}") from e
     vp, i64, u32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32
     lib.hpdct_version.restype = ctypes.c_char_p
+    lib.hpdct_build_info.restype = ctypes.c_char_p
+    lib.hpdct_decode_i8_f32.argtypes = [vp, vp, i64, vp]
+    lib.hpdct_decode_i8_f32.restype = ctypes.c_int
     lib.hpdct_status_string.restype = ctypes.c_char_p
     lib.hpdct_status_string.argtypes = [ctypes.c_int]
     lib.hpdct_last_error_string.restype = ctypes.c_char_p
@@ -157,6 +160,19 @@ def _check(status: int) -> None:
 
 def version() -> str:
     return load_library().hpdct_version().decode()
+
+
+def build_info() -> str:
+    """'src=<sha256 of csrc/ + include/> git=<rev> arch=gfx950' stamped at build
+    time (src_digest.py)."""
+    return load_library().hpdct_build_info().decode()
+
+
+def provenance() -> dict:
+    """The loaded library's build stamp and whether it matches the sources of
+    this tree (bench.py / smoke() report it)."""
+    import src_digest
+    return src_digest.provenance(build_info())
 
 
 def set_mapping(name: str) -> None:
@@ -583,6 +599,19 @@ def fill_hash_u8(out, seed: int, first_index: int = 0, stream=None):
     _device_plane(out, "out", None, 0, (_torch().uint8,))
     _check(load_library().hpdct_fill_hash_u8(ctypes.c_void_p(out.data_ptr()), out.numel(),
                                              ctypes.c_uint64(seed), first_index, _stream_ptr(stream)))
+    return out
+
+
+def decode_i8_f32(q, out=None, stream=None):
+    """int8 wire coefficients -> the fp32 coefficient plane (HIP kernel,
+    hpdct_decode_i8_f32): equal in value to the fp32 forward's output."""
+    torch = _torch()
+    _device_plane(q, "q", None, 0, (torch.int8,))
+    if out is None:
+        out = torch.empty(q.shape, dtype=torch.float32, device=q.device)
+    _device_plane(out, "out", q.device, q.numel(), (torch.float32,))
+    _check(load_library().hpdct_decode_i8_f32(ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                              q.numel(), _stream_ptr(stream)))
     return out
 
 

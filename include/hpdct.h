@@ -77,6 +77,10 @@ typedef enum hpdct_dtype {
 
 /* Library / error information. */
 const char* hpdct_version(void);
+/* Build provenance: "src=<sha256 of csrc/ + include/> git=<rev> arch=gfx950"
+ * (cuda-dct-idct_amd/src_digest.py defines the digest; bench.py recomputes it
+ * from the tree it runs in).  No reference counterpart. */
+const char* hpdct_build_info(void);
 const char* hpdct_status_string(hpdct_status status);
 const char* hpdct_last_error_string(void); /* thread-local, last failing call */
 
@@ -211,6 +215,14 @@ hpdct_status hpdct_stream_destroy(hpdct_stream_ctx ctx);
  * i of the frame = splitmix64(seed, first_index + i) & 255 (the oracle's
  * oracle_fill_hash_u8 restates it). */
 hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_t first_index, void* stream);
+
+/* Decode n int8 wire coefficients (hpdct_forward's HPDCT_I8 output, e.g. a
+ * root's gathered C4 frame) into the fp32 coefficient plane
+ * dct_all_blocks_cuda produces (main_newAppr.cu:252-291): out[i] = (float)q[i].
+ * Equal in value to the fp32 forward's output; a -0.0 of that output decodes
+ * as +0.0.  Device pointers: d_q 4-byte, d_out 16-byte aligned.  Async on
+ * `stream`.  No reference counterpart (the reference has no int8 format). */
+hpdct_status hpdct_decode_i8_f32(const int8_t* d_q, float* d_out, int64_t n, void* stream);
 
 /* Work mapping of the kernels (new; the reference has one fixed decomposition
  * per program).  Output is bit-identical in every mapping; only speed differs.

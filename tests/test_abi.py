@@ -101,6 +101,17 @@ def test_version_and_status_strings(hp):
     assert L.hpdct_status_string(3).startswith(b"quantised")
 
 
+def test_build_provenance_matches_tree(hp):
+    """The library carries the digest of the csrc/ + include/ it was built from
+    (src_digest.py, stamped by the Makefile); a stale build (sources edited,
+    library not rebuilt) fails here, and bench.py / smoke() print the same
+    check on the GPU box."""
+    info = hp.build_info()
+    assert info.startswith("src=") and "arch=gfx950" in info
+    prov = hp.provenance()
+    assert prov["lib_matches_sources"] is True, prov
+
+
 def test_tables_match_reference(hp, oracle):
     assert np.array_equal(hp.default_transform().view(np.uint32), oracle.default_transform().view(np.uint32))
     assert np.array_equal(hp.default_quant_table(), oracle.default_quant())

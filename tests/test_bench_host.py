@@ -119,6 +119,19 @@ def test_world_size_mismatch_is_an_error(monkeypatch):
     assert bench.main() == 2
 
 
+def test_nccl_refuses_more_ranks_than_gpus():
+    """--backend nccl with WORLD_SIZE > visible GPUs (0 here) exits 2 with a
+    clear message before any process group, RCCL or HIP call (VERDICT r3 item
+    5); gloo is the way to rehearse several ranks on fewer GPUs."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "nccl"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "one GPU per rank" in out.stderr and "WORLD_SIZE=2" in out.stderr
+    assert out.stdout.strip() == ""
+
+
 def test_sustained_phase_reports_the_slowest_rank_rate():
     """The sustained headline phase (a GPU-busy period long enough for an
     outside sampler) launches in chunks until its wall time is spent and

@@ -84,6 +84,64 @@ def test_world1_comm_from_unique_id(hp, dev):
         c.destroy()
 
 
+def test_world1_unique_id_comm_checks_each_new_geometry(hp, dev):
+    """A per-process communicator runs the geometry agreement all-reduce
+    (hpdct_dist_geometry.hpp) before the first gather of every new
+    (height, width, type, root), then gathers payload only: fp32, int8 and
+    again fp32 at one size, then a second size, all correct."""
+    import torch
+    c = hp.Comm.init_rank(1, hp.comm_unique_id(), 0, dev.index)
+    try:
+        for (h, w) in ((256, 512), (256, 512), (64, 1024)):
+            x = torch.empty((h, w), dtype=torch.uint8, device=dev)
+            hp.fill_hash_u8(x, seed=h + w)
+            for dt in (torch.float32, torch.int8, torch.float32):
+                slab = hp.forward(x, out_dtype=dt)
+                frame = torch.zeros_like(slab)
+                hp.gather_rows(c, slab, frame, h, w, root=0)
+                torch.cuda.synchronize()
+                assert torch.equal(frame, slab)
+    finally:
+        c.destroy()
+
+
+def test_world1_root_slab_in_place_is_a_no_op(hp, dev, comm1):
+    """The root's slab computed in place in the frame (bench C4 leg): at world
+    1 the gather moves nothing and leaves the frame as computed."""
+    import torch
+    x = torch.empty((512, 1024), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=9)
+    frame = torch.empty((512, 1024), dtype=torch.float32, device=dev)
+    hp.forward_slab(comm1, x, frame, 512, 1024)
+    hp.gather_rows(comm1, frame, frame, 512, 1024, root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(frame.view(torch.int32), hp.forward(x).view(torch.int32))
+
+
+@pytest.mark.parametrize("n", [1024 * 1024, 4096 * 4096 + 8, 1000, 0])
+def test_decode_int8_to_fp32(hp, dev, n):
+    """The root-side decode of the int8 wire format (hpdct_decode_i8_f32):
+    out = (float)q for every int8 value, whole 1 KiB wave blocks and a
+    ragged tail."""
+    import torch
+    q = torch.randint(-128, 128, (n,), dtype=torch.int8, device=dev)
+    out = torch.full((n,), 7.0, dtype=torch.float32, device=dev)
+    hp.decode_i8_f32(q, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, q.float())
+
+
+def test_decode_equals_fp32_forward_by_value(hp, dev):
+    import torch
+    x = torch.empty((2048, 4096), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=21)
+    q8 = hp.forward(x, out_dtype=torch.int8)
+    f = hp.forward(x)
+    d = hp.decode_i8_f32(q8)
+    torch.cuda.synchronize()
+    assert torch.equal(d, f)  # value equality: -0.0 in f decodes as +0.0
+
+
 def test_world1_gather_rejects_bad_root(hp, dev, comm1):
     import torch
     s = torch.empty((64, 64), dtype=torch.float32, device=dev)
@@ -121,4 +179,9 @@ def test_bench_nccl_process_group_at_world_size_1(tmp_path):
     assert c4["gather_path"].startswith("native RCCL"), c4
     assert c4["sharded_equals_unsharded"] is True
     assert c4["int8_wire_equals_fp32"] is True
+    for k in (2, 4, 8):
+        assert c4[f"predicted_compute_speedup_{k}"] > 0 and line[f"c4_predicted_compute_speedup_{k}"] > 0
+    assert c4["gather_bytes_to_root"] == 0 and c4["gather_ms"] < 1.0
+    assert c4["end_to_end_ms"] > 0 and c4["end_to_end_int8_ms"] > 0 and c4["decode_int8_ms"] > 0
     assert line["parity_spot_check"] is True
+    assert line["provenance"]["lib_matches_sources"] is True

@@ -239,9 +239,11 @@ def test_forward_nonfinite_fp32_input(hp, oracle, dev):
 def test_fp32_input_quotient_range_check(hp, oracle, dev, lo, hi):
     """fp32 input over three coefficient ranges: every |C| within the 3-op
     quotient's verified |C| <= 4096 (pixel values), a mix, and mostly beyond
-    it (a range-checked fast quotient was measured for fp32 input and not
-    kept; fp32 input divides with IEEE division).
-    Bit-exact with the built-in and with the caller's T."""
+    it.  fp32 input with an integer 1..255 table takes the checked 3-op
+    quotient per output row in the duo kernels (kVarFastDivChecked): rows
+    whose |C| all stay <= 4096 use it, any other row IEEE division, so the
+    three ranges drive both branches.  Bit-exact with the built-in and with
+    the caller's T."""
     import torch
     img = np.random.default_rng(7).uniform(lo, hi, (256, 1024)).astype(np.float32)
     if lo == 0.0:
@@ -515,6 +517,31 @@ def test_capped_packed_forward_large_frames(hp, oracle, dev, h, w, qtab):
             hp.set_quant_table(None)
     ref = oracle.fdct(img) if Q is None else oracle.fdct(img, Q=Q)
     assert bits_equal(got, ref), mismatches(got, ref)
+
+
+def test_capped_duo_writebacks_large_frame(hp, oracle, dev):
+    """fp32 frames of >= 64 duo waves per CU (here 4096 x 8200: 524,800 tiles,
+    16,400 waves of 32 tiles on 256 CUs) take the one-wave, residency-capped
+    duo kernels (hpdct_launch.hpp DuoShape): the rows-first forward with the
+    X-128 write-back, the rows-first inverse with the q*Q write-back and the
+    reference-order inverse with the q*Q write-back.  Ragged width (tiles_x =
+    1025).  Bit-exact, the write-back planes included."""
+    h, w = 4096, 8200
+    img = oracle.hash_u8(h * w, seed=77).reshape(h, w).astype(np.float32)
+    x = to_dev(img, dev)
+    q = hp.forward(x, row_first=True, writeback_shift=True)
+    q_ref = oracle.fdct(img, row_first=True)
+    assert bits_equal(to_host(q), q_ref), mismatches(to_host(q), q_ref)
+    assert bits_equal(to_host(x), img - np.float32(128))
+    dq_ref = q_ref * np.tile(oracle.default_quant().astype(np.float32), (h // 8, w // 8))
+    qd = q.clone()
+    r = hp.inverse(qd, row_first=True, writeback_dequant=True)
+    assert bits_equal(to_host(r), oracle.idct(q_ref, row_first=True))
+    assert bits_equal(to_host(qd), dq_ref)
+    qd = q.clone()
+    r = hp.inverse(qd, writeback_dequant=True)
+    assert bits_equal(to_host(r), oracle.idct(q_ref))
+    assert bits_equal(to_host(qd), dq_ref)
 
 
 # --------------------------------------------------------------------- full-size configs

@@ -58,7 +58,7 @@ enum : unsigned {
     kVarFiniteSkip = 1u << 18,  // fp32 input, built-in T: per-wave finiteness test of the loaded tiles;
                                 // all finite -> the zero terms of T are skipped (exact: a chain from +0
                                 // never holds -0), otherwise the full chain (0*inf, 0*NaN -> NaN)
-    // (1u << 26: free; a translation-touch variant measured there in round 2 gave no gain)
+    // (1u << 26: the product's kVarFastDivChecked)
     // diagnostics only (tools/kbench): split the kernel's time into its phases
     kVarNoLoad = 1u << 27,      // tile bytes synthesised from the lane id instead of loaded
     kVarXcdSwz = 1u << 29,      // XCD-contiguous workgroup order: the hardware deals workgroups round-robin
@@ -71,6 +71,12 @@ enum : unsigned {
                                 // 32 B per lane; launched only for such widths (the branch costs the
                                 // power-of-two frames ~3 %, profiles/r01/ab_straddle.log)     // int8 rows stored only when ntiles == 0xffffffff (never): loads + math
 };
+// the tools-only A/B bits never alias a product-only bit
+static_assert(((kVarPersist | kVarXorCvt | kVarRowMajor | kVarLdsSwz | kVarLdsLoad | kVarNTLoad | kVarPersist2 |
+                kVarTwoSets | kVarStSc1 | kVarStSc0Sc1 | kVarFiniteSkip | kVarNoLoad | kVarXcdSwz | kVarNoStore |
+                kVarPanel | (15u << 8)) &
+               hpdct::kProductOnlyVarBits) == 0,
+              "a tools A/B variant bit aliases a product-only kernel variant bit");
 template <unsigned kVar>
 constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
 template <unsigned kVar>
