@@ -6,12 +6,12 @@
 namespace hpdct {
 template <>
 hipError_t launch_fdct_frames<float>(const FrameTable<float>& ft, int n, const TileGrid& g, const QParams& q,
-                                     bool fd, hipStream_t s) {
+                                     int fd, hipStream_t s) {
     return launch_fdct_frames_impl<float>(ft, n, g, q, fd, s);
 }
 template <>
 hipError_t launch_fdct_frames<int8_t>(const FrameTable<int8_t>& ft, int n, const TileGrid& g, const QParams& q,
-                                      bool fd, hipStream_t s) {
+                                      int fd, hipStream_t s) {
     return launch_fdct_frames_impl<int8_t>(ft, n, g, q, fd, s);
 }
 }  // namespace hpdct

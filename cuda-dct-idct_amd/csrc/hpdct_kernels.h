@@ -29,13 +29,16 @@ struct TileGrid {
     uint64_t width;  // elements per image row
 };
 
-// fastdiv: use the 3-operation quotient (only legal for uint8 input, the
-// built-in T and a table whose entries are all integers in 1..255; the
-// caller checks).  shift is 128 (reference level shift) or 0.
+// qmode (the quotient): 0 IEEE division; 1 the 3-operation quotient (only
+// legal for a table whose entries are all integers in 1..255 with uint8 input
+// and the built-in T, or fp32 input behind the duo kernels' range check; the
+// caller checks); 2 as 1 plus the default JPEG table's per-position 3-op forms
+// (hpdct_quant_forms.h: only the default table, uint8 input, built-in T,
+// shift 128).  shift is 128 (reference level shift) or 0.
 // row_first: cublasDCTv2 pass order (fp32 -> fp32 only).
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                       const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s);
+                       const QParams& q, float shift, int qmode, bool row_first, hipStream_t s);
 
 // dq_out (fp32 -> fp32 with dequantisation only, else nullptr): q*Q is also
 // written there (the in-place multiply of the cublasDCTv2 inverse).
@@ -57,7 +60,7 @@ enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
 // kRtReconNone.  Zeroes *sums on the stream before the kernel.
 // zero_sums: hipMemsetAsync the sums before the kernel (else they accumulate)
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
-                            const TileGrid& g, const QParams& qp, bool fast, bool zero_sums, hipStream_t s);
+                            const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s);
 
 // A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch
 // device pointer pairs travel in the kernel arguments (1 KiB).
@@ -68,9 +71,9 @@ struct FrameTable {
     TOut* out[kMaxFramesPerLaunch];
 };
 // n <= kMaxFramesPerLaunch frames of grid g, uint8 -> TOut (float or int8_t),
-// built-in T, quantised with q (fastdiv as launch_fdct).
+// built-in T, quantised with q (qmode as launch_fdct).
 template <typename TOut>
-hipError_t launch_fdct_frames(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, bool fastdiv,
+hipError_t launch_fdct_frames(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, int qmode,
                               hipStream_t s);
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);

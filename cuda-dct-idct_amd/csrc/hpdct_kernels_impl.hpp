@@ -20,6 +20,7 @@
 #pragma once
 
 #include "hpdct_kernels.h"
+#include "hpdct_quant_forms.h"
 #include "hpdct_tile.hpp"
 
 namespace hpdct {
@@ -46,6 +47,10 @@ enum : unsigned {
                               // (fdct_tile_pk; 844 instead of 1,308 VALU instructions per set)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
+    kVarJpegQ = 1u << 11,     // the DEFAULT JPEG table, uint8 input, built-in T, level shift 128 (with
+                              // kVarFastDiv): per position the 3-op form F or H where it is proven exact
+                              // below that position's |C| bound, the 6-op form elsewhere
+                              // (hpdct_quant_forms.h, tests/tools/verify_quant_pos.c)
     kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
                               // multiple of 512 px) stores two contiguous runs per instruction instead of
                               // 32 B per lane; launched only for such widths (the branch costs the
@@ -53,7 +58,7 @@ enum : unsigned {
 };
 // Bits only the product kernels give a meaning to: the tools' A/B variant
 // bits must stay clear of them (static_assert in tools/kbench_variants.hpp).
-constexpr unsigned kProductOnlyVarBits = kVarFastDivChecked;
+constexpr unsigned kProductOnlyVarBits = kVarFastDivChecked | kVarJpegQ;
 template <unsigned kVar>
 constexpr uint32_t kBlock = ((kVar >> 12) & 3u) == 1u   ? 64u
                             : ((kVar >> 12) & 3u) == 2u ? 512u
@@ -105,6 +110,14 @@ __device__ __forceinline__ uint32_t pack_u8x4(float a, float b, float c, float d
 __device__ __forceinline__ float signed_half(float x) {
     return __uint_as_float(
         __builtin_amdgcn_bitop3_b32(0x7fffffffu, __float_as_uint(0.49999997f), __float_as_uint(x), 0xca));
+}
+
+// copysign(kMag, x) for a compile-time magnitude, one v_bitop3_b32
+template <int kPos>
+__device__ __forceinline__ float signed_bias(float x) {
+    constexpr float kMag = quantforms::jpeg_bias(kPos);
+    return __uint_as_float(
+        __builtin_amdgcn_bitop3_b32(0x7fffffffu, __float_as_uint(kMag), __float_as_uint(x), 0xca));
 }
 
 // roundf (round half away from zero) in three operations:
@@ -177,6 +190,40 @@ __device__ __forceinline__ float quantise(float c, float q, float r) {
         d = c / q;  // IEEE (hipcc default: correctly rounded fp32 division)
     }
     return round_half_away(d);
+}
+
+// divide_matrices at table position kPos (= v * 8 + u), returned BEFORE the
+// final truncation (the caller truncates: v_trunc_f32 for fp32 output, the
+// truncating int8 convert for the wire format).  With kVarJpegQ the
+// position's proven 3-op form where there is one (F or H), else the quotient
+// (verified 3-op or IEEE) plus the signed 0.49999997 of the 3-op roundf.
+template <unsigned kVar, int kPos>
+__device__ __forceinline__ float quantise_biased_at(float c, float q, float r) {
+    if constexpr ((kVar & kVarJpegQ) != 0 && quantforms::jpeg_form(kPos) != quantforms::kFull) {
+        (void)q;
+        return __builtin_fmaf(c, r, signed_bias<kPos>(c));
+    } else {
+        const float d = quotient<kVar>(c, q, r);
+        return d + signed_half(d);
+    }
+}
+template <unsigned kVar, int kPos>
+__device__ __forceinline__ float quantise_at(float c, float q, float r) {
+    return __builtin_truncf(quantise_biased_at<kVar, kPos>(c, q, r));
+}
+
+// int8 bytes of four already-biased values (truncating convert straight into
+// each byte, SDWA dst_sel)
+__device__ __forceinline__ uint32_t pack_biased_i8x4(float a, float b, float c, float d) {
+    uint32_t w;
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD" : "=v"(w) : "v"(a));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(b));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(c));
+    asm volatile("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+                 : "+v"(w) : "v"(d));
+    return w;
 }
 
 // divide_matrices for one output row of 8 values per lane, kVarFastDivChecked:
@@ -487,13 +534,16 @@ __device__ __forceinline__ void fdct_tile_body(const RawTile<TIn>& raw, const Ti
     }
     auto emit = [&](auto v, float (&c)[8]) {
         if constexpr (kQuant && std::is_same_v<TOut, int8_t> && (kVar & kVarI8Pack) != 0) {
-            unroll<8>([&](auto u) { c[u] = quotient<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
-            const uint2 w = make_uint2(pack_q_i8x4(c[0], c[1], c[2], c[3]), pack_q_i8x4(c[4], c[5], c[6], c[7]));
+            unroll<8>([&](auto u) {
+                c[u] = quantise_biased_at<kVar, v * 8 + u>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]);
+            });
+            const uint2 w =
+                make_uint2(pack_biased_i8x4(c[0], c[1], c[2], c[3]), pack_biased_i8x4(c[4], c[5], c[6], c[7]));
             st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
             return;
         }
         if constexpr (kQuant) {
-            unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+            unroll<8>([&](auto u) { c[u] = quantise_at<kVar, v * 8 + u>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
         }
         sink(v, p, ok, seg, c);
     };
@@ -505,14 +555,15 @@ __device__ __forceinline__ void fdct_tile_body(const RawTile<TIn>& raw, const Ti
 }
 
 // Packed-fp32 forward of uint8 pixels with the built-in T, quantised to fp32
-// (kVarPacked).  quot2(v, k, c2) returns the quotient pair of output columns
-// (pair_u(k, 0), pair_u(k, 1)) of row v.  The kernels define quot2 themselves
+// (kVarPacked).  bquot2(v, k, c2) returns the biased quotient pair (before the
+// truncation) of output columns (pair_u(k, 0), pair_u(k, 1)) of row v.  The
+// kernels define bquot2 themselves
 // over their own QParams argument: handing the QParams to a device function
 // by reference made hipcc keep the quotient operands in scratch memory
 // (364 B per lane, 4x slower).
-template <unsigned kVar, typename Quot2>
+template <unsigned kVar, typename BQuot2>
 __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img, float* __restrict__ out,
-                                                 const TileGrid& g, float shift, Quot2&& quot2) {
+                                                 const TileGrid& g, float shift, BQuot2&& bquot2) {
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, float> sink{out, g.width, slots};
     walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
@@ -525,9 +576,7 @@ __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img
         fdct_tile_pk(x2, [&](auto v, f32x2(&c2)[4]) {
             float c[8];
             unroll<4>([&](auto k) {
-                // round half away: trunc(d + copysign(0.49999997, d)) (verify_round3.c)
-                f32x2 d2 = quot2(v, k, c2[k]);
-                d2 = d2 + f32x2{__builtin_copysignf(0.49999997f, d2.x), __builtin_copysignf(0.49999997f, d2.y)};
+                const f32x2 d2 = bquot2(v, k, c2[k]);
                 c[pair_u(k, 0)] = __builtin_truncf(d2.x);
                 c[pair_u(k, 1)] = __builtin_truncf(d2.y);
             });
@@ -536,19 +585,32 @@ __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img
     });
 }
 
-// C / Q for one pair of output columns: the verified 3-op quotient per half,
-// or IEEE division (a generic lambda in each kernel, over its own QParams)
-#define HPDCT_PK_QUOT2(kVar, qp)                                                                   \
+// round(C / Q) for one pair of output columns, before the truncation: with
+// kVarJpegQ and a proven 3-op form at BOTH positions one packed fma with a
+// per-half signed bias; otherwise the verified 3-op quotient per half (or
+// IEEE division) and the signed 0.49999997 of the 3-op roundf
+// (verify_round3.c).  A generic lambda in each kernel, over its own QParams.
+#define HPDCT_PK_BQUOT2(kVar, qp)                                                                  \
     [&](auto v, auto k, f32x2 c2) -> f32x2 {                                                       \
         constexpr int u0 = pair_u(k, 0), u1 = pair_u(k, 1);                                        \
-        const f32x2 q2 = {qp.q.v[v * 8 + u0], qp.q.v[v * 8 + u1]};                                 \
-        if constexpr (((kVar) & kVarFastDiv) != 0) {                                               \
-            const f32x2 r2 = {qp.r.v[v * 8 + u0], qp.r.v[v * 8 + u1]};                             \
-            const f32x2 q0 = c2 * r2;                                                              \
-            const f32x2 e = fma2(-q0, q2, c2);                                                     \
-            return fma2(e, r2, q0);                                                                \
+        constexpr int p0 = v * 8 + u0, p1 = v * 8 + u1;                                            \
+        const f32x2 q2 = {qp.q.v[p0], qp.q.v[p1]};                                                 \
+        if constexpr (((kVar) & kVarJpegQ) != 0 && quantforms::jpeg_form(p0) != quantforms::kFull && \
+                      quantforms::jpeg_form(p1) != quantforms::kFull) {                            \
+            (void)q2;                                                                              \
+            const f32x2 r2 = {qp.r.v[p0], qp.r.v[p1]};                                             \
+            return fma2(c2, r2, f32x2{signed_bias<p0>(c2.x), signed_bias<p1>(c2.y)});              \
         } else {                                                                                   \
-            return f32x2{c2.x / q2.x, c2.y / q2.y};                                                \
+            f32x2 d2;                                                                              \
+            if constexpr (((kVar) & kVarFastDiv) != 0) {                                           \
+                const f32x2 r2 = {qp.r.v[p0], qp.r.v[p1]};                                         \
+                const f32x2 q0 = c2 * r2;                                                          \
+                const f32x2 e = fma2(-q0, q2, c2);                                                 \
+                d2 = fma2(e, r2, q0);                                                              \
+            } else {                                                                               \
+                d2 = f32x2{c2.x / q2.x, c2.y / q2.y};                                              \
+            }                                                                                      \
+            return d2 + f32x2{__builtin_copysignf(0.49999997f, d2.x), __builtin_copysignf(0.49999997f, d2.y)}; \
         }                                                                                          \
     }
 
@@ -574,7 +636,7 @@ __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __rest
                                                             const float* __restrict__ t_dev, QParams qp, float shift) {
     if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float> &&
                   kBuiltinT && kQuant && !kWriteback && (kVar & kVarRowFirst) == 0) {
-        fdct_packed_body<kVar>(img, out, g, shift, HPDCT_PK_QUOT2(kVar, qp));
+        fdct_packed_body<kVar>(img, out, g, shift, HPDCT_PK_BQUOT2(kVar, qp));
     } else {
         fdct_body<TIn, TOut, kQuant, kBuiltinT, kWriteback, kVar>(img, out, shifted, g, t_dev, qp, shift);
     }
@@ -589,7 +651,7 @@ template <typename TOut, unsigned kVar>
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_frames_kernel(FrameTable<TOut> ft, TileGrid g, QParams qp) {
     const uint32_t f = blockIdx.y;
     if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TOut, float>) {
-        fdct_packed_body<kVar>(ft.in[f], ft.out[f], g, 128.0f, HPDCT_PK_QUOT2(kVar, qp));
+        fdct_packed_body<kVar>(ft.in[f], ft.out[f], g, 128.0f, HPDCT_PK_BQUOT2(kVar, qp));
     } else {
         fdct_body<uint8_t, TOut, true, true, false, kVar>(ft.in[f], ft.out[f], nullptr, g, nullptr, qp, 128.0f);
     }

@@ -235,7 +235,11 @@ hipError_t rowfirst_duo_go(const float* src, float* out, float* wb, const TileGr
 
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
-                            const QParams& q, float shift, bool fastdiv, bool row_first, hipStream_t s) {
+                            const QParams& q, float shift, int qmode, bool row_first, hipStream_t s) {
+    const bool fastdiv = qmode != 0;
+    // the default JPEG table's per-position forms: tile kernels (the octet
+    // mapping of small frames keeps the verified quotient everywhere)
+    const bool jpeg = qmode == 2;
     constexpr unsigned kBase = kProdVar<TIn, TOut>;
     constexpr unsigned kOct = kOctVar<TOut>;
     constexpr bool kFastDivOk = std::is_same_v<TIn, uint8_t> && kQuant && kBuiltinT && !kWriteback;
@@ -277,6 +281,9 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
     if constexpr (kStraddleOk) {
         if (g.tiles_x % 64u != 0u) {
             if constexpr (kFastDivOk) {
+                if (jpeg)
+                    return fdct_tile_go<kBase | kVarFastDiv | kVarJpegQ | kVarStraddle, TIn, TOut, kQuant, kBuiltinT,
+                                        kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
                 if (fastdiv)
                     return fdct_tile_go<kBase | kVarFastDiv | kVarStraddle, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
                         img, out, shifted, g, t_dev, q, shift, s);
@@ -286,11 +293,15 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
         }
     }
     if constexpr (kFastDivOk) {
+        if (jpeg)
+            return fdct_tile_go<kBase | kVarFastDiv | kVarJpegQ, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+                img, out, shifted, g, t_dev, q, shift, s);
         if (fastdiv)
             return fdct_tile_go<kBase | kVarFastDiv, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev,
                                                                                           q, shift, s);
     }
     (void)fastdiv;
+    (void)jpeg;
     return fdct_tile_go<kBase, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
 }
 
@@ -400,15 +411,19 @@ hipError_t fdct_frames_go(const FrameTable<TOut>& ft, int n, const TileGrid& g, 
 }
 
 template <typename TOut>
-hipError_t launch_fdct_frames_impl(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q,
-                                   bool fastdiv, hipStream_t s) {
+hipError_t launch_fdct_frames_impl(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, int qmode,
+                                   hipStream_t s) {
     constexpr unsigned kBase = kProdVar<uint8_t, TOut>;
+    constexpr unsigned kJ = kVarFastDiv | kVarJpegQ;
     if constexpr (std::is_same_v<TOut, float>) {
         if (g.tiles_x % 64u != 0u)
-            return fastdiv ? fdct_frames_go<kBase | kVarFastDiv | kVarStraddle>(ft, n, g, q, s)
-                           : fdct_frames_go<kBase | kVarStraddle>(ft, n, g, q, s);
+            return qmode == 2   ? fdct_frames_go<kBase | kJ | kVarStraddle>(ft, n, g, q, s)
+                   : qmode == 1 ? fdct_frames_go<kBase | kVarFastDiv | kVarStraddle>(ft, n, g, q, s)
+                                : fdct_frames_go<kBase | kVarStraddle>(ft, n, g, q, s);
     }
-    return fastdiv ? fdct_frames_go<kBase | kVarFastDiv>(ft, n, g, q, s) : fdct_frames_go<kBase>(ft, n, g, q, s);
+    return qmode == 2   ? fdct_frames_go<kBase | kJ>(ft, n, g, q, s)
+           : qmode == 1 ? fdct_frames_go<kBase | kVarFastDiv>(ft, n, g, q, s)
+                        : fdct_frames_go<kBase>(ft, n, g, q, s);
 }
 
 inline hipError_t launch_fill_hash_impl(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s) {

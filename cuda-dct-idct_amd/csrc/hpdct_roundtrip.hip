@@ -3,7 +3,7 @@
 
 namespace hpdct {
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
-                            const TileGrid& g, const QParams& qp, bool fast, bool zero_sums, hipStream_t s) {
+                            const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s) {
     return launch_roundtrip_impl(img, coef, recon, recon_kind, sums, g, qp, fast, s, zero_sums);
 }
 }  // namespace hpdct

@@ -69,14 +69,17 @@ constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
 // struct.  Measured alternatives (round 3, profiles/r03/kb_rt16.log, 8192^2):
 // one struct per workgroup (no two workgroups on one line) 78.4-78.8 us
 // against 79.7 us; per-wave atomics 607 us.
-template <int kRecon, bool kStats, bool kFast, int kRaw = 2, bool kStraddle = false>
+// kQMode: 0 IEEE division (kFast false), 1 the verified 3-op quotient (kFast),
+// 2 as 1 with the default JPEG table's per-position 3-op forms (kVarJpegQ).
+template <int kRecon, bool kStats, int kQMode, int kRaw = 2, bool kStraddle = false>
 __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
                                                                           RtSums* __restrict__ sums, TileGrid g,
                                                                           QParams qp) {
-    constexpr unsigned kVar =
-        (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) | (kStraddle ? kVarStraddle : 0u);
+    constexpr bool kFast = kQMode != 0;
+    constexpr unsigned kVar = (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) |
+                              (kQMode == 2 ? kVarJpegQ : 0u) | (kStraddle ? kVarStraddle : 0u);
     // built-in T.  The forward's u8 pixels are finite, so the zero terms of T
     // are skipped exactly; so are the inverse's for kFast (int8-range q times
     // Q in 1..255).  With IEEE division and a caller's table, q = round(C/Q)
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
         uint2 q8[8];
         float qf[kFast ? 1 : 8][8];
         fdct_tile(T, x, [&](auto v, float (&c)[8]) {
-            unroll<8>([&](auto u) { c[u] = quantise<kVar>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
+            unroll<8>([&](auto u) { c[u] = quantise_at<kVar, v * 8 + u>(c[u], qp.q.v[v * 8 + u], qp.r.v[v * 8 + u]); });
             coef_sink(v, p, ok, seg, c);
             if constexpr (kFast) {
                 // c holds integers in [-127, 127]: the truncating convert is exact
@@ -218,34 +221,41 @@ inline dim3 roundtrip_grid(const TileGrid& g) {
 }
 
 namespace rt_detail {
-template <int kRecon, bool kStats, bool kFast>
+template <int kRecon, bool kStats, int kQMode>
 hipError_t go(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
               hipStream_t s) {
-    if constexpr (kFast) {
+    if constexpr (kQMode != 0) {
         if (g.tiles_x % 64u != 0u) {  // straddling sets: two-run staged stores (kVarStraddle)
-            hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kFast, 2, true>), roundtrip_grid(g), dim3(512), 0, s,
-                               img, coef, recon, sums, g, qp);
+            hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode, 2, true>), roundtrip_grid(g), dim3(512), 0,
+                               s, img, coef, recon, sums, g, qp);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kFast>), roundtrip_grid(g), dim3(512), 0, s, img, coef,
+    hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode>), roundtrip_grid(g), dim3(512), 0, s, img, coef,
                        recon, sums, g, qp);
     return hipGetLastError();
 }
+template <int kRecon, bool kStats>
+hipError_t go_q(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
+                int qmode, hipStream_t s) {
+    switch (qmode) {
+        case 2: return go<kRecon, kStats, 2>(img, coef, recon, sums, g, qp, s);
+        case 1: return go<kRecon, kStats, 1>(img, coef, recon, sums, g, qp, s);
+        default: return go<kRecon, kStats, 0>(img, coef, recon, sums, g, qp, s);
+    }
+}
 template <int kRecon>
 hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g, const QParams& qp,
-                bool fast, hipStream_t s) {
-    if (sums) {
-        return fast ? go<kRecon, true, true>(img, coef, recon, sums, g, qp, s)
-                    : go<kRecon, true, false>(img, coef, recon, sums, g, qp, s);
-    }
-    return fast ? go<kRecon, false, true>(img, coef, recon, sums, g, qp, s)
-                : go<kRecon, false, false>(img, coef, recon, sums, g, qp, s);
+                int qmode, hipStream_t s) {
+    if (sums) return go_q<kRecon, true>(img, coef, recon, sums, g, qp, qmode, s);
+    return go_q<kRecon, false>(img, coef, recon, sums, g, qp, qmode, s);
 }
 }  // namespace rt_detail
 
+// fast: 0 IEEE division, 1 the verified 3-op quotient, 2 with the default
+// JPEG table's per-position forms (hpdct_kernels.h launch_roundtrip)
 inline hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
-                                        RtSums* sums, const TileGrid& g, const QParams& qp, bool fast,
+                                        RtSums* sums, const TileGrid& g, const QParams& qp, int fast,
                                         hipStream_t s, bool zero_sums = true) {
     if (sums && zero_sums) {
         const hipError_t e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);

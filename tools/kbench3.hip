@@ -252,6 +252,21 @@ void prod_f32_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL(k, grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s,
                        static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
 }
+// the library's int8 forward kernel, capped at kWg workgroups per CU (0: uncapped)
+template <unsigned kVar, uint32_t kWg>
+void prod_i8_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = hpdct::fdct_kernel<uint8_t, int8_t, true, true, false, kVar>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    hipLaunchKernelGGL(k, grid_for(c.g, false, c.cus, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s,
+                       static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
+}
+// C3 round trip with a quotient mode (1: verified 3-op, 2: + JPEG per-position forms)
+template <bool kStats, int kQMode>
+void rt_q(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+                       static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
+}
 // C3 round trip (512-thread workgroups), capped at kWg workgroups per CU (0: uncapped)
 template <bool kStats, uint32_t kWg>
 void rt_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
@@ -313,6 +328,8 @@ int main(int argc, char** argv) {
     constexpr unsigned F = kVarFastDiv;
     constexpr unsigned P = kProdVar<uint8_t, float> | F;
     constexpr unsigned I8 = kProdVar<uint8_t, int8_t> | F;
+    // the headline's capped variant (one-wave workgroups, packed transform)
+    constexpr unsigned PK1 = (P & ~(3u << 12)) | kOneWaveWg | kVarPacked;
     std::vector<Variant> vars = {
         {"fwd", "fwd u8->f32 library (b512)", prod_f32_fwd<P>, 5, 4, true},
         {"fwd", "fwd u8->f32 dma 8w x 2/cu", dma_f32_fwd<8, 2>, 5, 4, true},
@@ -460,6 +477,28 @@ int main(int argc, char** argv) {
         {"dropin", "dropin fwd f32 duo b64 cap 10 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 10>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo b64 cap 12 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 12>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo library again", dropin_fwd_cap<kDuoVar, 0>, 12, 4, true},
+        // round 4: the default JPEG table's per-position 3-op quantiser forms (kVarJpegQ) against the
+        // verified 6-op form, in the product's dispatch, and the headline cap re-swept with them
+        {"jq", "fwd u8->f32 library cap 10 (6-op)", prod_f32_fwd_cap<PK1, 10>, 5, 4, true},
+        {"jq", "fwd u8->f32 jpegq cap 8 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 8>, 5, 4, true},
+        {"jq", "fwd u8->f32 jpegq cap 9 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 9>, 5, 4, true},
+        {"jq", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jq", "fwd u8->f32 jpegq cap 12 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 12>, 5, 4, true},
+        {"jq", "fwd u8->f32 library cap 10 (6-op) again", prod_f32_fwd_cap<PK1, 10>, 5, 4, true},
+        {"jq", "fwd u8->f32 jpegq cap 10 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jqi8", "fwd u8->i8 library b512 (6-op)", prod_i8_fwd<I8>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq b512", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq b256", prod_i8_fwd<(I8 & ~(3u << 12)) | kVarJpegQ>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq b1024", prod_i8_fwd<(I8 & ~(3u << 12)) | (3u << 12) | kVarJpegQ>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq b64 cap 16 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 16>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 library b512 (6-op) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq b512 again", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
+        {"jqrt", "rt + sums, library (6-op)", rt_q<true, 1>, 6, 1, true},
+        {"jqrt", "rt + sums, jpegq", rt_q<true, 2>, 6, 1, true},
+        {"jqrt", "rt no sums, library (6-op)", rt_q<false, 1>, 6, 1, true},
+        {"jqrt", "rt no sums, jpegq", rt_q<false, 2>, 6, 1, true},
+        {"jqrt", "rt + sums, library (6-op) again", rt_q<true, 1>, 6, 1, true},
+        {"jqrt", "rt + sums, jpegq again", rt_q<true, 2>, 6, 1, true},
         {"pat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"pat", "pat band 4 w/cu", pat_band_go<4, false>, 5, 4, false},
         {"pat", "pat band 4 w/cu prefetch", pat_band_go<4, true>, 5, 4, false},
@@ -492,7 +531,7 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin";
+               v.group == "dropin" || v.group == "jqrt";
     });
     if (want_coef) {
         g_img = img;

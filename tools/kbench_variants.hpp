@@ -15,7 +15,7 @@
 //   kVarPacked                  packed-fp32 (v_pk_fma_f32) transform
 //   kVarFiniteSkip              zero-term skip for finite fp32 tiles
 //   kVarXcdSwz / kVarPanel      XCD-contiguous / column-panel set orders
-//   bits 8..11                  minimum waves per SIMD for the register allocator
+//   bits 8..10                  minimum waves per SIMD for the register allocator
 //   kVarNoLoad / kVarNoStore    diagnostics: phase split of the kernel time
 #pragma once
 
@@ -38,7 +38,7 @@ enum : unsigned {
     kVarRowMajor = 32u,  // forward: finish each P row and its C row before the next (fewer live VGPRs?)
     kVarLdsSwz = 64u,    // LDS re-staging with the slot swizzle k ^ ((k >> 3) & 1): conflict-free deposits
     kVarLdsLoad = 128u,  // fp32 inputs: 1 KiB-contiguous row loads, re-staged through LDS into the tile layout
-    // bits 8..11: minimum waves per SIMD requested from the register allocator (0 = compiler default)
+    // bits 8..10: minimum waves per SIMD requested from the register allocator (0 = compiler default)
     // bits 12..13: workgroup size: 0 -> 256 threads, 1 -> 64, 2 -> 512, 3 -> 1024
     kVarRowFirst = 1u << 14,  // cublasDCTv2 pass order (row pass first), fp32 compat path
     kVarWbDequant = 1u << 15, // inverse: write q*Q back into the fp32 coefficient input
@@ -74,11 +74,11 @@ enum : unsigned {
 // the tools-only A/B bits never alias a product-only bit
 static_assert(((kVarPersist | kVarXorCvt | kVarRowMajor | kVarLdsSwz | kVarLdsLoad | kVarNTLoad | kVarPersist2 |
                 kVarTwoSets | kVarStSc1 | kVarStSc0Sc1 | kVarFiniteSkip | kVarNoLoad | kVarXcdSwz | kVarNoStore |
-                kVarPanel | (15u << 8)) &
+                kVarPanel | (7u << 8)) &
                hpdct::kProductOnlyVarBits) == 0,
               "a tools A/B variant bit aliases a product-only kernel variant bit");
 template <unsigned kVar>
-constexpr unsigned kMinWaves = ((kVar >> 8) & 15u) ? ((kVar >> 8) & 15u) : 1u;
+constexpr unsigned kMinWaves = ((kVar >> 8) & 7u) ? ((kVar >> 8) & 7u) : 1u;  // bit 11: the product's kVarJpegQ
 template <unsigned kVar>
 constexpr uint32_t kBlock = ((kVar >> 12) & 3u) == 1u   ? 64u
                             : ((kVar >> 12) & 3u) == 2u ? 512u
