@@ -3,13 +3,20 @@
 // frames streamed H2D / D2H).  The reference has no equivalent: its drivers
 // do one blocking cudaMemcpy each way per image (benchmark_newAppr.cu:88,97).
 //
-// Pipeline: frame f goes to stream f % nstreams, which owns one device input
-// and one device output buffer; on that stream: H2D copy -> fused forward
-// kernel -> D2H copy.  Streams run concurrently, so the H2D DMA of one frame,
-// the kernel of another and the D2H DMA of a third overlap; a stream's own
-// operations are ordered, which makes its buffer reuse safe.  Host buffers
-// should be pinned (hipHostMalloc / torch pin_memory) for the copies to be
-// asynchronous and overlap.
+// Pipeline ("engines", the default): one in-order HIP stream per engine --
+// H2D copies, forward kernels, D2H copies -- over a device ring of `slots`
+// (the API's nstreams) input/output buffer pairs.  Frame f uses slot
+// f % slots; events order it across the engines:
+//   H2D(f)    after kernel(f - slots) has consumed the slot's input,
+//   kernel(f) after H2D(f) and after D2H(f - slots) has drained the output,
+//   D2H(f)    after kernel(f).
+// Each DMA direction then sees one ordered queue of whole-frame copies, so
+// the two directions run full duplex and the kernels hide between them.
+// The round-1..3 layout ("streams": frame f on stream f % nstreams doing its
+// own H2D -> kernel -> D2H) is kept behind HPDCT_STREAM_PIPELINE=streams for
+// A/B timing; there the copies of different streams interleave on the DMA
+// engines.  Host buffers should be pinned (hipHostMalloc / torch pin_memory)
+// for the copies to be asynchronous and overlap.
 //
 // The streams, device ring and timing events live in an hpdct_stream_ctx
 // (hpdct_stream_create / _run / _destroy), so a caller that streams many
@@ -17,6 +24,8 @@
 // form (create, run, destroy).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <new>
 #include <string>
 #include <vector>
@@ -28,15 +37,20 @@ struct hpdct_stream_ctx_s {
     int64_t height = 0, width = 0;
     hpdct_dtype out_type = HPDCT_F32;
     int device = -1;
-    std::vector<hipStream_t> streams;
-    std::vector<void*> in, out;
-    std::vector<hipEvent_t> done;  // per stream: its last operation of a batch
+    bool engines = true;              // one stream per engine over a slot ring (else one per slot)
+    std::vector<hipStream_t> streams;  // engines: {H2D, kernels, D2H}; else one per slot
+    std::vector<void*> in, out;        // the device ring, one pair per slot
+    std::vector<hipEvent_t> done;      // streams layout: per stream, its last operation of a batch
+    std::vector<hipEvent_t> loaded, computed, drained;  // engines layout: per slot
     hipEvent_t t0 = nullptr, t1 = nullptr;
 
     ~hpdct_stream_ctx_s() {
         for (void* p : in) (void)hipFree(p);
         for (void* p : out) (void)hipFree(p);
         for (hipEvent_t e : done) (void)hipEventDestroy(e);
+        for (hipEvent_t e : loaded) (void)hipEventDestroy(e);
+        for (hipEvent_t e : computed) (void)hipEventDestroy(e);
+        for (hipEvent_t e : drained) (void)hipEventDestroy(e);
         if (t0) (void)hipEventDestroy(t0);
         if (t1) (void)hipEventDestroy(t1);
         for (hipStream_t s : streams) (void)hipStreamDestroy(s);
@@ -72,8 +86,28 @@ hpdct_status create(hpdct_stream_ctx* out_ctx, int64_t height, int64_t width, hp
     c->out_type = out_type;
     const size_t px = static_cast<size_t>(height) * static_cast<size_t>(width);
     const size_t out_bytes = px * (out_type == HPDCT_F32 ? 4 : 1);
+    const char* layout = getenv("HPDCT_STREAM_PIPELINE");
+    c->engines = !(layout && strcmp(layout, "streams") == 0);
     hipError_t he = hipGetDevice(&c->device);
-    for (int s = 0; s < nstreams && he == hipSuccess; ++s) {
+    if (c->engines) {
+        for (int k = 0; k < 3 && he == hipSuccess; ++k) {
+            hipStream_t st;
+            if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) == hipSuccess) c->streams.push_back(st);
+        }
+        for (int s = 0; s < nstreams && he == hipSuccess; ++s) {
+            void *di = nullptr, *dout = nullptr;
+            if ((he = hipMalloc(&di, px)) != hipSuccess) break;
+            c->in.push_back(di);
+            if ((he = hipMalloc(&dout, out_bytes)) != hipSuccess) break;
+            c->out.push_back(dout);
+            for (auto* v : {&c->loaded, &c->computed, &c->drained}) {
+                hipEvent_t ev;
+                if ((he = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
+                v->push_back(ev);
+            }
+        }
+    }
+    for (int s = 0; s < nstreams && he == hipSuccess && !c->engines; ++s) {
         hipStream_t st;
         void *di = nullptr, *dout = nullptr;
         hipEvent_t ev;
@@ -93,6 +127,45 @@ hpdct_status create(hpdct_stream_ctx* out_ctx, int64_t height, int64_t width, hp
         return device_fail(he, "creating the streams / device ring");
     }
     *out_ctx = c;
+    return HPDCT_SUCCESS;
+}
+
+// the engines layout (see the file comment)
+hpdct_status run_engines(hpdct_stream_ctx c, const uint8_t* const* h_frames, void* const* h_coef, int64_t n_frames,
+                         float* elapsed_ms, size_t px, size_t out_bytes) {
+    hipStream_t h2d = c->streams[0], comp = c->streams[1], d2h = c->streams[2];
+    const int64_t slots = static_cast<int64_t>(c->in.size());
+    hipError_t e = hipEventRecord(c->t0, h2d);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comp, c->t0, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(d2h, c->t0, 0);
+    for (int64_t f = 0; f < n_frames && e == hipSuccess; ++f) {
+        const int64_t s = f % slots;
+        const bool reuse = f >= slots;  // the slot held frame f - slots
+        if (reuse) e = hipStreamWaitEvent(h2d, c->computed[s], 0);  // its input consumed
+        if (e == hipSuccess) e = hipMemcpyAsync(c->in[s], h_frames[f], px, hipMemcpyHostToDevice, h2d);
+        if (e == hipSuccess) e = hipEventRecord(c->loaded[s], h2d);
+        if (e == hipSuccess) e = hipStreamWaitEvent(comp, c->loaded[s], 0);
+        if (e == hipSuccess && reuse) e = hipStreamWaitEvent(comp, c->drained[s], 0);  // its output drained
+        if (e != hipSuccess) break;
+        const hpdct_status hs =
+            hpdct_forward(c->in[s], HPDCT_U8, c->out[s], c->out_type, c->height, c->width, nullptr, 0u, comp);
+        if (hs != HPDCT_SUCCESS) {
+            for (hipStream_t x : c->streams) (void)hipStreamSynchronize(x);
+            return hs;
+        }
+        e = hipEventRecord(c->computed[s], comp);
+        if (e == hipSuccess) e = hipStreamWaitEvent(d2h, c->computed[s], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(h_coef[f], c->out[s], out_bytes, hipMemcpyDeviceToHost, d2h);
+        if (e == hipSuccess) e = hipEventRecord(c->drained[s], d2h);
+    }
+    // the last D2H is the batch's last operation (D2H copies are in frame order)
+    if (e == hipSuccess) e = hipEventRecord(c->t1, d2h);
+    if (e == hipSuccess) e = hipEventSynchronize(c->t1);
+    float ms = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->t0, c->t1);
+    for (hipStream_t st : c->streams) (void)hipStreamSynchronize(st);
+    if (e != hipSuccess) return device_fail(e, "copy/compute pipeline");
+    if (elapsed_ms) *elapsed_ms = ms;
     return HPDCT_SUCCESS;
 }
 
@@ -117,6 +190,7 @@ hpdct_status run(hpdct_stream_ctx c, const uint8_t* const* h_frames, void* const
     const int64_t height = c->height, width = c->width;
     const size_t px = static_cast<size_t>(height) * static_cast<size_t>(width);
     const size_t out_bytes = px * (c->out_type == HPDCT_F32 ? 4 : 1);
+    if (c->engines) return run_engines(c, h_frames, h_coef, n_frames, elapsed_ms, px, out_bytes);
     const int nstreams = static_cast<int>(c->streams.size());
     // start marker: every stream waits for it, so the timed region holds the whole batch
     hipError_t e = hipEventRecord(c->t0, c->streams[0]);
