@@ -43,8 +43,8 @@ enum : unsigned {
                                     // output row when every lane's 8 values have |C| <= 4096 (wave-uniform
                                     // test, NaN/inf fail it), IEEE division otherwise: exact either way
                                     // (verify_fastdiv covers every |C| <= 4096)
-    kVarPacked = 1u << 19,    // uint8 -> fp32 quantised, built-in T: packed-fp32 transform and quotient
-                              // (fdct_tile_pk; 844 instead of 1,308 VALU instructions per set)
+    kVarPacked = 1u << 19,    // uint8 -> fp32 or int8 quantised, built-in T: packed-fp32 transform and
+                              // quotient (fdct_tile_pk; fp32: 844 instead of 1,308 VALU instructions per set)
     kVarI8Pack = 1u << 17,    // int8 output: round-half-away folded into the truncating cvt, and each
                               // coefficient converted straight into its byte (SDWA dst_sel, one op)
     kVarJpegQ = 1u << 11,     // the DEFAULT JPEG table, uint8 input, built-in T, level shift 128 (with
@@ -561,11 +561,11 @@ __device__ __forceinline__ void fdct_tile_body(const RawTile<TIn>& raw, const Ti
 // over their own QParams argument: handing the QParams to a device function
 // by reference made hipcc keep the quotient operands in scratch memory
 // (364 B per lane, 4x slower).
-template <unsigned kVar, typename BQuot2>
-__device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img, float* __restrict__ out,
+template <unsigned kVar, typename TOut, typename BQuot2>
+__device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img, TOut* __restrict__ out,
                                                  const TileGrid& g, float shift, BQuot2&& bquot2) {
     float4* const slots = wave_slots<kVar>();
-    const RowSink<kVar, float> sink{out, g.width, slots};
+    const RowSink<kVar, float> sink{reinterpret_cast<float*>(out), g.width, slots};
     walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
         float xs[8][8];
         raw.to_float(xs, 0.0f);
@@ -577,10 +577,18 @@ __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img
             float c[8];
             unroll<4>([&](auto k) {
                 const f32x2 d2 = bquot2(v, k, c2[k]);
-                c[pair_u(k, 0)] = __builtin_truncf(d2.x);
-                c[pair_u(k, 1)] = __builtin_truncf(d2.y);
+                c[pair_u(k, 0)] = d2.x;
+                c[pair_u(k, 1)] = d2.y;
             });
-            sink(v, p, ok, seg, c);
+            if constexpr (std::is_same_v<TOut, int8_t>) {
+                // the truncating int8 convert straight into each byte (wire format)
+                const uint2 w =
+                    make_uint2(pack_biased_i8x4(c[0], c[1], c[2], c[3]), pack_biased_i8x4(c[4], c[5], c[6], c[7]));
+                st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
+            } else {
+                unroll<8>([&](auto u) { c[u] = __builtin_truncf(c[u]); });
+                sink(v, p, ok, seg, c);
+            }
         });
     });
 }
@@ -634,9 +642,10 @@ template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteb
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_kernel(const TIn* __restrict__ img, TOut* __restrict__ out,
                                                             float* __restrict__ shifted, TileGrid g,
                                                             const float* __restrict__ t_dev, QParams qp, float shift) {
-    if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, float> &&
-                  kBuiltinT && kQuant && !kWriteback && (kVar & kVarRowFirst) == 0) {
-        fdct_packed_body<kVar>(img, out, g, shift, HPDCT_PK_BQUOT2(kVar, qp));
+    if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TIn, uint8_t> &&
+                  (std::is_same_v<TOut, float> || std::is_same_v<TOut, int8_t>) && kBuiltinT && kQuant &&
+                  !kWriteback && (kVar & kVarRowFirst) == 0) {
+        fdct_packed_body<kVar, TOut>(img, out, g, shift, HPDCT_PK_BQUOT2(kVar, qp));
     } else {
         fdct_body<TIn, TOut, kQuant, kBuiltinT, kWriteback, kVar>(img, out, shifted, g, t_dev, qp, shift);
     }
@@ -651,7 +660,7 @@ template <typename TOut, unsigned kVar>
 __global__ __launch_bounds__(kBlock<kVar>, 1) void fdct_frames_kernel(FrameTable<TOut> ft, TileGrid g, QParams qp) {
     const uint32_t f = blockIdx.y;
     if constexpr ((kVar & kVarPacked) != 0 && std::is_same_v<TOut, float>) {
-        fdct_packed_body<kVar>(ft.in[f], ft.out[f], g, 128.0f, HPDCT_PK_BQUOT2(kVar, qp));
+        fdct_packed_body<kVar, TOut>(ft.in[f], ft.out[f], g, 128.0f, HPDCT_PK_BQUOT2(kVar, qp));
     } else {
         fdct_body<uint8_t, TOut, true, true, false, kVar>(ft.in[f], ft.out[f], nullptr, g, nullptr, qp, 128.0f);
     }

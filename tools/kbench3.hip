@@ -491,6 +491,9 @@ int main(int argc, char** argv) {
         {"jqi8", "fwd u8->i8 jpegq b256", prod_i8_fwd<(I8 & ~(3u << 12)) | kVarJpegQ>, 2, 1, true},
         {"jqi8", "fwd u8->i8 jpegq b1024", prod_i8_fwd<(I8 & ~(3u << 12)) | (3u << 12) | kVarJpegQ>, 2, 1, true},
         {"jqi8", "fwd u8->i8 jpegq b64 cap 16 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 16>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq packed b512", prod_i8_fwd<I8 | kVarJpegQ | kVarPacked>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq packed b256", prod_i8_fwd<(I8 & ~(3u << 12)) | kVarJpegQ | kVarPacked>, 2, 1, true},
+        {"jqi8", "fwd u8->i8 jpegq packed b64 cap 16 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 16>, 2, 1, true},
         {"jqi8", "fwd u8->i8 library b512 (6-op) again", prod_i8_fwd<I8>, 2, 1, true},
         {"jqi8", "fwd u8->i8 jpegq b512 again", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
         {"jqrt", "rt + sums, library (6-op)", rt_q<true, 1>, 6, 1, true},
