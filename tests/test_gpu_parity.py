@@ -544,6 +544,62 @@ def test_capped_duo_writebacks_large_frame(hp, oracle, dev):
     assert bits_equal(to_host(qd), dq_ref)
 
 
+def _hardest_tiles(oracle, per_pos=6, n_tiles=1 << 18, seed=11):
+    """Tiles whose unquantised coefficient C at some position (v, u) lies
+    closest to a rounding boundary (k + 1/2) * Q of the default table, found by
+    the oracle among n_tiles random tiles, plus each position's two
+    extreme tiles (|C| at that position's bound): the inputs where a quotient
+    form that is not exact would show.  One row of tiles, 8 x (8 * count)."""
+    rng = np.random.default_rng(seed)
+    w = 8 * n_tiles
+    img = rng.integers(0, 256, (8, w), dtype=np.uint8)
+    c = oracle.fdct(img, quant=False).reshape(8, n_tiles, 8).transpose(1, 0, 2).reshape(n_tiles, 64)
+    q = oracle.default_quant().reshape(64).astype(np.float64)
+    frac = np.abs(np.abs(c.astype(np.float64)) / q - np.floor(np.abs(c.astype(np.float64)) / q) - 0.5)
+    pick = set()
+    for p in range(64):
+        pick.update(np.argsort(frac[:, p], kind="stable")[:per_pos].tolist())
+    tiles = [img[:, 8 * t:8 * t + 8] for t in sorted(pick)]
+    T = oracle.default_transform().astype(np.float64)
+    for v in range(8):
+        for u in range(8):
+            s = np.sign(np.outer(T[v], T[u]))
+            for sign in (1, -1):
+                tiles.append(np.where(sign * s > 0, 255, 0).astype(np.uint8))
+    while len(tiles) % 64:  # whole 64-tile sets: a 512-px multiple width
+        tiles.append(rng.integers(0, 256, (8, 8), dtype=np.uint8))
+    return np.ascontiguousarray(np.concatenate(tiles, axis=1))
+
+
+@pytest.fixture(scope="module")
+def hardest(oracle):
+    img = _hardest_tiles(oracle)
+    return img, oracle.fdct(img)
+
+
+def test_quantiser_hardest_tiles(hp, dev, hardest):
+    """The default JPEG table's per-position quantiser forms (kVarJpegQ,
+    hpdct_quant_forms.h) and the 6-op form on the tiles nearest a rounding
+    boundary at every position and on the extreme tiles: fp32 and int8
+    output bit-exact against the oracle's IEEE division + roundf, in every
+    mapping (the tile kernels are the ones with the forms)."""
+    import torch
+    img, ref = hardest
+    x = to_dev(img, dev)
+    assert bits_equal(to_host(hp.forward(x)), ref), mismatches(to_host(hp.forward(x)), ref)
+    got8 = to_host(hp.forward(x, out_dtype=torch.int8))
+    assert np.array_equal(got8.astype(np.float32), ref)
+    # the same tiles in a frame large enough for the capped packed kernel (> 16 sets per CU)
+    h = 8 * (-(-(17 * 256 * 64 * 64) // img.size))
+    big = np.ascontiguousarray(np.tile(img, (h // 8, 1)))
+    refb = np.tile(ref, (h // 8, 1))
+    xb = to_dev(big, dev)
+    assert bits_equal(to_host(hp.forward(xb)), refb)
+    assert np.array_equal(to_host(hp.forward(xb, out_dtype=torch.int8)).astype(np.float32), refb)
+    coef, rec, _ = hp.roundtrip(xb, sums=True)
+    assert bits_equal(to_host(coef), refb)
+
+
 # --------------------------------------------------------------------- full-size configs
 def test_c2_1024_bitexact(hp, oracle, dev, golden):
     img = oracle.rand_u8(1024 * 1024).reshape(1024, 1024)

@@ -20,6 +20,9 @@
 #   pmctcc:<args>         TCC/TA counter pass over kbench3 <args>
 #   verify_quant:<xmax>   tests/tools/verify_quant1 (exhaustive quantiser proof)
 #   devinfo               HIP device attributes the launch code reads
+#   pmctraffic            HBM bytes of the path's kernels: tools/pmc_traffic.sh (FETCH_SIZE and
+#                         WRITE_SIZE in separate passes + calibration), parsed into
+#                         <out>/pmc_traffic.json by tools/pmc_parse.py
 # The session stops at the first step that faults, aborts or times out (exit
 # >= 2 or a signal); a plain test failure (pytest exit 1) lets later steps run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -78,6 +81,9 @@ for s in "$@"; do
     pmctcc) pmc "tcc_${p[4]}_${p[1]}" "$TCC" "${p[@]:1}" || exit $? ;;
     verify_quant) step "verify_quant1_${p[1]:-4096}" 300 tests/tools/verify_quant1 "${p[1]:-4096}" || exit $? ;;
     devinfo) step devinfo 120 python3 tools/devinfo.py || exit $? ;;
+    pmctraffic)
+        step pmc_traffic 900 tools/pmc_traffic.sh || exit $?
+        python3 tools/pmc_parse.py gpurun_out/pmc "$OUT/pmc_traffic.json" > "$OUT/pmc_parse.log" 2>&1 || true ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done
