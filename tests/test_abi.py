@@ -212,6 +212,20 @@ def test_bad_shapes_rejected_before_device_work(hp, h, w):
     assert st == 1
 
 
+def test_decode_arguments_rejected(hp):
+    """hpdct_decode_i8_f32 validates before any device work: n == 0 is a no-op
+    (NULL allowed), NULL / negative / misaligned pointers are rejected."""
+    L = hp.load_library()
+    a, b = ctypes.c_void_p(1 << 20), ctypes.c_void_p(1 << 30)
+    assert L.hpdct_decode_i8_f32(None, None, 0, None) == 0
+    assert L.hpdct_decode_i8_f32(None, b, 64, None) == 1
+    assert L.hpdct_decode_i8_f32(a, None, 64, None) == 1
+    assert L.hpdct_decode_i8_f32(a, b, -1, None) == 1
+    assert L.hpdct_decode_i8_f32(ctypes.c_void_p((1 << 20) + 2), b, 64, None) == 1
+    assert L.hpdct_decode_i8_f32(a, ctypes.c_void_p((1 << 30) + 8), 64, None) == 1
+    assert b"aligned" in L.hpdct_last_error_string()
+
+
 def test_bad_arguments_rejected(hp):
     L = hp.load_library()
     a, b = ctypes.c_void_p(1 << 20), ctypes.c_void_p(1 << 30)

@@ -496,6 +496,23 @@ int main(int argc, char** argv) {
         {"jqi8", "fwd u8->i8 jpegq packed b64 cap 16 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 16>, 2, 1, true},
         {"jqi8", "fwd u8->i8 library b512 (6-op) again", prod_i8_fwd<I8>, 2, 1, true},
         {"jqi8", "fwd u8->i8 jpegq b512 again", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
+        // round 4, session 2: the packed int8 forward (JPEG forms and the 6-op quotient) across block sizes / caps
+        {"jqi8b", "fwd u8->i8 library b512 (6-op)", prod_i8_fwd<I8>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 packed 6-op b512", prod_i8_fwd<I8 | kVarPacked>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b512", prod_i8_fwd<I8 | kVarJpegQ | kVarPacked>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b1024", prod_i8_fwd<(I8 & ~(3u << 12)) | (3u << 12) | kVarJpegQ | kVarPacked>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b64 cap 8 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 8>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b64 cap 12 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 12>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b64 cap 20 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 20>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b64 uncapped", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 0>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 library b512 (6-op) again", prod_i8_fwd<I8>, 2, 1, true},
+        {"jqi8b", "fwd u8->i8 jpegq packed b512 again", prod_i8_fwd<I8 | kVarJpegQ | kVarPacked>, 2, 1, true},
+        // the headline cap below 8 with the JPEG forms (fewer VALU per set)
+        {"jqf", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jqf", "fwd u8->f32 jpegq cap 6 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 6>, 5, 4, true},
+        {"jqf", "fwd u8->f32 jpegq cap 7 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        {"jqf", "fwd u8->f32 jpegq cap 8 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 8>, 5, 4, true},
+        {"jqf", "fwd u8->f32 jpegq cap 10 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
         {"jqrt", "rt + sums, library (6-op)", rt_q<true, 1>, 6, 1, true},
         {"jqrt", "rt + sums, jpegq", rt_q<true, 2>, 6, 1, true},
         {"jqrt", "rt no sums, library (6-op)", rt_q<false, 1>, 6, 1, true},
