@@ -85,9 +85,13 @@ size_t static_lds_of(K kern) {
 // re-staging with non-temporal stores (1 KiB contiguous per store
 // instruction), 8-bit planes with non-temporal stores; the int8 output with
 // the SDWA byte-pack conversion; the fast quotient where the caller proved it
-// legal.  512-thread workgroups (1-3 % faster than 256 on every kernel).
+// legal.  512-thread workgroups (1-3 % faster than 256 on every kernel in
+// round 1), except the int8 output: 256-thread workgroups since its JPEG-form
+// quantiser (round 4: 8192^2 28.9 against 29.8-30.0 us with 512,
+// profiles/r04/a/kb3_jqi8_8192.log).
 template <typename TIn, typename TOut>
-constexpr unsigned kProdVar = (2u << 12) | kVarNT | (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
+constexpr unsigned kProdVar = (std::is_same_v<TOut, int8_t> ? 0u : (2u << 12)) | kVarNT |
+                              (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
                               (std::is_same_v<TOut, int8_t> ? kVarI8Pack : 0u);
 // Octet kernels (hpdct_octet.hpp, 8 lanes per tile) for smaller frames,
 // where the tile-per-lane grid is too short to fill 256 CUs (1024^2: 6.2 ->

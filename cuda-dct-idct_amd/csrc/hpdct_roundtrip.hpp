@@ -71,14 +71,17 @@ constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
 // against 79.7 us; per-wave atomics 607 us.
 // kQMode: 0 IEEE division (kFast false), 1 the verified 3-op quotient (kFast),
 // 2 as 1 with the default JPEG table's per-position 3-op forms (kVarJpegQ).
-template <int kRecon, bool kStats, int kQMode, int kRaw = 2, bool kStraddle = false>
-__global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
+// kBlock: threads per workgroup (512 in the product; A/B in tools/kbench3 "jqrt")
+template <int kRecon, bool kStats, int kQMode, int kRaw = 2, bool kStraddle = false, int kBlock = 512>
+__global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
                                                                           RtSums* __restrict__ sums, TileGrid g,
                                                                           QParams qp) {
     constexpr bool kFast = kQMode != 0;
-    constexpr unsigned kVar = (2u << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) |
+    static_assert(kBlock == 256 || kBlock == 512 || kBlock == 1024, "workgroup size");
+    constexpr unsigned kBlockBits = kBlock == 256 ? 0u : kBlock == 512 ? 2u : 3u;
+    constexpr unsigned kVar = (kBlockBits << 12) | kVarNT | kVarLdsStore | (kFast ? kVarFastDiv : 0u) |
                               (kQMode == 2 ? kVarJpegQ : 0u) | (kStraddle ? kVarStraddle : 0u);
     // built-in T.  The forward's u8 pixels are finite, so the zero terms of T
     // are skipped exactly; so are the inverse's for kFast (int8-range q times
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
 
     uint2* stash = nullptr;  // kRaw == 2: this wave's [row][lane] pixel words
     if constexpr (kStats && kRaw == 2) {
-        __shared__ uint2 raw_lds[512 / 64][8 * 64];
+        __shared__ uint2 raw_lds[kBlock / 64][8 * 64];
         stash = raw_lds[__builtin_amdgcn_readfirstlane(threadIdx.x / 64u)];
     }
     const uint32_t lane = threadIdx.x & 63u;
@@ -198,13 +201,13 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
         f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
         // a wave's f is < 64 * 2^40: bit 63 of its slot carries the wave's flag
         if (__builtin_amdgcn_ballot_w64(!f_ok) != 0) f |= kRtSseF32Invalid;
-        __shared__ unsigned long long part[512 / 64][3];
+        __shared__ unsigned long long part[kBlock / 64][3];
         const uint32_t w = threadIdx.x / 64u;
         if ((threadIdx.x & 63u) == 0u) part[w][0] = f, part[w][1] = e8, part[w][2] = xx;
         __syncthreads();
         if (threadIdx.x < 3u) {
             unsigned long long s = 0, bad = 0;
-            for (uint32_t k = 0; k < 512u / 64u; ++k) {
+            for (uint32_t k = 0; k < kBlock / 64u; ++k) {
                 s += part[k][threadIdx.x] & ~kRtSseF32Invalid;
                 bad |= part[k][threadIdx.x] & kRtSseF32Invalid;
             }
@@ -215,9 +218,9 @@ __global__ __launch_bounds__(512, kRtWaves<kRecon>) void roundtrip_kernel(const 
     }
 }
 
-inline dim3 roundtrip_grid(const TileGrid& g) {
-    const uint32_t sets = (g.ntiles + 63u) / 64u;
-    return dim3((sets + 7u) / 8u);
+inline dim3 roundtrip_grid(const TileGrid& g, uint32_t block = 512) {
+    const uint32_t sets = (g.ntiles + 63u) / 64u, waves = block / 64u;
+    return dim3((sets + waves - 1u) / waves);
 }
 
 namespace rt_detail {

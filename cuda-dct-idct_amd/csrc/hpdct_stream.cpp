@@ -3,20 +3,25 @@
 // frames streamed H2D / D2H).  The reference has no equivalent: its drivers
 // do one blocking cudaMemcpy each way per image (benchmark_newAppr.cu:88,97).
 //
-// Pipeline ("engines", the default): one in-order HIP stream per engine --
-// H2D copies, forward kernels, D2H copies -- over a device ring of `slots`
-// (the API's nstreams) input/output buffer pairs.  Frame f uses slot
-// f % slots; events order it across the engines:
-//   H2D(f)    after kernel(f - slots) has consumed the slot's input,
-//   kernel(f) after H2D(f) and after D2H(f - slots) has drained the output,
-//   D2H(f)    after kernel(f).
-// Each DMA direction then sees one ordered queue of whole-frame copies, so
-// the two directions run full duplex and the kernels hide between them.
-// The round-1..3 layout ("streams": frame f on stream f % nstreams doing its
-// own H2D -> kernel -> D2H) is kept behind HPDCT_STREAM_PIPELINE=streams for
-// A/B timing; there the copies of different streams interleave on the DMA
-// engines.  Host buffers should be pinned (hipHostMalloc / torch pin_memory)
-// for the copies to be asynchronous and overlap.
+// Pipeline ("streams", the product): frame f goes to stream f % nstreams,
+// which owns one device input and one device output buffer; on that stream:
+// H2D copy -> fused forward kernel -> D2H copy.  Streams run concurrently, so
+// the H2D DMA of one frame, the kernel of another and the D2H DMA of a third
+// overlap; a stream's own operations are ordered, which makes its buffer reuse
+// safe.  With 2 streams each DMA direction stays busy in steady state (a
+// stream's H2D of frame f + 2 follows its own D2H of frame f, which follows the
+// other stream's D2H): 0.97 (fp32) / 0.90 (int8) of the copy-only duplex
+// ceiling of the same bytes (profiles/r04/a/bench.json.log, extras.c5).
+//
+// HPDCT_STREAM_PIPELINE=engines selects an A/B layout measured in round 4 and
+// rejected: one in-order stream per engine (H2D copies, kernels, D2H copies)
+// over a ring of nstreams device slots, ordered by per-slot events (H2D(f)
+// after kernel(f - slots), kernel(f) after H2D(f) and D2H(f - slots), D2H(f)
+// after kernel(f)).  It is bit-exact but ran at 213-440 fp32 / 1,580-1,630
+// int8 frames/s against 784 / 2,542 for the product: on this ROCm the
+// cross-stream event waits in front of every copy serialise the pipeline.
+// Host buffers should be pinned (hipHostMalloc / torch pin_memory) for the
+// copies to be asynchronous and overlap.
 //
 // The streams, device ring and timing events live in an hpdct_stream_ctx
 // (hpdct_stream_create / _run / _destroy), so a caller that streams many
@@ -37,7 +42,7 @@ struct hpdct_stream_ctx_s {
     int64_t height = 0, width = 0;
     hpdct_dtype out_type = HPDCT_F32;
     int device = -1;
-    bool engines = true;              // one stream per engine over a slot ring (else one per slot)
+    bool engines = false;             // A/B: one stream per engine over a slot ring (else one per slot)
     std::vector<hipStream_t> streams;  // engines: {H2D, kernels, D2H}; else one per slot
     std::vector<void*> in, out;        // the device ring, one pair per slot
     std::vector<hipEvent_t> done;      // streams layout: per stream, its last operation of a batch
@@ -87,7 +92,7 @@ hpdct_status create(hpdct_stream_ctx* out_ctx, int64_t height, int64_t width, hp
     const size_t px = static_cast<size_t>(height) * static_cast<size_t>(width);
     const size_t out_bytes = px * (out_type == HPDCT_F32 ? 4 : 1);
     const char* layout = getenv("HPDCT_STREAM_PIPELINE");
-    c->engines = !(layout && strcmp(layout, "streams") == 0);
+    c->engines = layout && strcmp(layout, "engines") == 0;
     hipError_t he = hipGetDevice(&c->device);
     if (c->engines) {
         for (int k = 0; k < 3 && he == hipSuccess; ++k) {

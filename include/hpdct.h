@@ -186,12 +186,11 @@ hpdct_status hpdct_forward_frames(const uint8_t* const* d_images, void* const* d
 
 /* Host-resident batch (BASELINE config C5): frame f (height x width uint8 at
  * h_frames[f]) -> coefficients at h_coef[f] (out_type HPDCT_F32 or HPDCT_I8),
- * pipelined through a device ring of nstreams (1..16) input/output buffer
- * pairs ("slots"): one in-order HIP stream per engine (H2D copies, forward
- * kernels, D2H copies) ordered by per-slot events, so the H2D copy, the kernel
- * and the D2H copy of different frames overlap and both DMA directions run
- * full duplex.  (HPDCT_STREAM_PIPELINE=streams selects the round-1..3 layout,
- * one stream per slot doing its own H2D -> kernel -> D2H, for A/B timing.)
+ * pipelined over nstreams (1..16) HIP streams, each with one device input and
+ * one output buffer: H2D copy, fused forward kernel and D2H copy of different
+ * frames overlap (2 streams keep both DMA directions busy: 0.90-0.97 of the
+ * copy-only duplex ceiling on MI355X).  HPDCT_STREAM_PIPELINE=engines selects
+ * a rejected A/B layout (one stream per engine over nstreams device slots).
  * Pointers may repeat (a pool cycled over the batch).  Host
  * buffers should be pinned for the copies to overlap.  Synchronous: returns
  * when every coefficient plane is in host memory; *elapsed_ms (may be NULL)
@@ -202,8 +201,8 @@ hpdct_status hpdct_stream_forward(const uint8_t* const* h_frames, void* const* h
                                   float* elapsed_ms);
 
 /* The same pipeline with its resources kept across calls: hpdct_stream_create
- * makes the streams, the nstreams device input/output buffer pairs (one
- * height x width frame each) and the events on the current device;
+ * makes the nstreams HIP streams, their device input/output buffers (one
+ * height x width frame each) and the timing events on the current device;
  * hpdct_stream_run streams one batch through them (semantics and timing as
  * hpdct_stream_forward, on the context's device); hpdct_stream_destroy frees
  * them.  hpdct_stream_forward is create + run + destroy.  A context is not

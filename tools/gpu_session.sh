@@ -19,6 +19,7 @@
 #   pmcsq:<args>          SQ/GRBM counter pass over kbench3 <args>
 #   pmctcc:<args>         TCC/TA counter pass over kbench3 <args>
 #   verify_quant:<xmax>   tests/tools/verify_quant1 (exhaustive quantiser proof)
+#   kbd[:<args>]          tools/kb_decode (int8 -> fp32 decode A/B)
 #   devinfo               HIP device attributes the launch code reads
 #   pmctraffic            HBM bytes of the path's kernels: tools/pmc_traffic.sh (FETCH_SIZE and
 #                         WRITE_SIZE in separate passes + calibration), parsed into
@@ -81,6 +82,7 @@ for s in "$@"; do
     pmctcc) pmc "tcc_${p[4]}_${p[1]}" "$TCC" "${p[@]:1}" || exit $? ;;
     verify_quant) step "verify_quant1_${p[1]:-4096}" 300 tests/tools/verify_quant1 "${p[1]:-4096}" || exit $? ;;
     devinfo) step devinfo 120 python3 tools/devinfo.py || exit $? ;;
+    kbd) step kb_decode 300 tools/kb_decode "${p[@]:1}" || exit $? ;;
     pmctraffic)
         step pmc_traffic 900 tools/pmc_traffic.sh || exit $?
         python3 tools/pmc_parse.py gpurun_out/pmc "$OUT/pmc_traffic.json" > "$OUT/pmc_parse.log" 2>&1 || true ;;

@@ -267,6 +267,13 @@ void rt_q(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
 }
+template <bool kStats, int kQMode, int kB>
+void rt_qb(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false, kB>), roundtrip_grid(c.g, kB), dim3(kB),
+                       0, s, static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g,
+                       c.qp);
+}
 // C3 round trip (512-thread workgroups), capped at kWg workgroups per CU (0: uncapped)
 template <bool kStats, uint32_t kWg>
 void rt_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
@@ -507,6 +514,30 @@ int main(int argc, char** argv) {
         {"jqi8b", "fwd u8->i8 jpegq packed b64 uncapped", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ | kVarPacked, 0>, 2, 1, true},
         {"jqi8b", "fwd u8->i8 library b512 (6-op) again", prod_i8_fwd<I8>, 2, 1, true},
         {"jqi8b", "fwd u8->i8 jpegq packed b512 again", prod_i8_fwd<I8 | kVarJpegQ | kVarPacked>, 2, 1, true},
+        // round 4, session 3: int8 block sizes with and without the JPEG forms; headline cap 7 vs 10 repeated
+        {"jqi8c", "fwd u8->i8 6-op b512", prod_i8_fwd<(I8 & ~(3u << 12)) | (2u << 12)>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 6-op b256", prod_i8_fwd<(I8 & ~(3u << 12))>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 jpegq b512", prod_i8_fwd<(I8 & ~(3u << 12)) | (2u << 12) | kVarJpegQ>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 jpegq b256", prod_i8_fwd<(I8 & ~(3u << 12)) | kVarJpegQ>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 jpegq b64 uncapped", prod_i8_fwd<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 6-op b256 again", prod_i8_fwd<(I8 & ~(3u << 12))>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 jpegq b256 again", prod_i8_fwd<(I8 & ~(3u << 12)) | kVarJpegQ>, 2, 1, true},
+        {"jqi8c", "fwd u8->i8 jpegq b512 again", prod_i8_fwd<(I8 & ~(3u << 12)) | (2u << 12) | kVarJpegQ>, 2, 1, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 7 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 9 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 9>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 10 w/cu b", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 7 w/cu b", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 10 w/cu c", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"jqcap", "fwd u8->f32 jpegq cap 7 w/cu c", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        // round trip workgroup size
+        {"jqrtb", "rt + sums, jpegq b512", rt_q<true, 2>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq b256", rt_qb<true, 2, 256>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq b1024", rt_qb<true, 2, 1024>, 6, 1, true},
+        {"jqrtb", "rt no sums, jpegq b512", rt_q<false, 2>, 6, 1, true},
+        {"jqrtb", "rt no sums, jpegq b256", rt_qb<false, 2, 256>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq b512 again", rt_q<true, 2>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq b256 again", rt_qb<true, 2, 256>, 6, 1, true},
         // the headline cap below 8 with the JPEG forms (fewer VALU per set)
         {"jqf", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
         {"jqf", "fwd u8->f32 jpegq cap 6 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 6>, 5, 4, true},
@@ -551,7 +582,7 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin" || v.group == "jqrt";
+               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb";
     });
     if (want_coef) {
         g_img = img;
