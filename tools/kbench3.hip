@@ -267,6 +267,13 @@ void rt_q(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
 }
+// the sums zeroed by three stream write-value commands instead of a memset
+template <int kQMode>
+void rt_wv(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    for (int k = 0; k < 3; ++k) (void)hipStreamWriteValue64(s, reinterpret_cast<uint64_t*>(g_sums) + k, 0ull, 0);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+                       static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, g_sums, c.g, c.qp);
+}
 template <bool kStats, int kQMode, int kB>
 void rt_qb(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
@@ -538,6 +545,8 @@ int main(int argc, char** argv) {
         {"jqrtb", "rt no sums, jpegq b256", rt_qb<false, 2, 256>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b512 again", rt_q<true, 2>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b256 again", rt_qb<true, 2, 256>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq, zeroed by write-value", rt_wv<2>, 6, 1, true},
+        {"jqrtb", "rt + sums, jpegq b512 again 2", rt_q<true, 2>, 6, 1, true},
         // the headline cap below 8 with the JPEG forms (fewer VALU per set)
         {"jqf", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
         {"jqf", "fwd u8->f32 jpegq cap 6 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 6>, 5, 4, true},
