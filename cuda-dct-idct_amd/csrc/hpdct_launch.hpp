@@ -41,7 +41,10 @@ inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t blo
 // gfx950 per MI355X_MICROARCH.md), so the caps keep their meaning on a part
 // with another LDS size.
 constexpr size_t kLdsPerCUDefault = 160u * 1024u;
-constexpr uint32_t kF32CapWavesPerCU = 10;
+// 10 in round 3; 7 since round 4: 56.9-57.1 against 57.7-58.4 us at 8192^2
+// with the per-position quantiser (profiles/r04/b/kb3_jqcap_8192.log; 6 waves
+// per CU: 64.8 us, profiles/r04/a/kb3_jqf_8192.log)
+constexpr uint32_t kF32CapWavesPerCU = 7;
 
 // A device attribute of the current device, cached per thread and device.
 template <hipDeviceAttribute_t kAttr>
@@ -136,7 +139,8 @@ hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g,
 //    about one round of resident waves: 1024-thread workgroups, no cap (4096^2:
 //    15.8 us against 17.9-18.8 capped; round 2: 2048 x 16384 35.2 -> 32.3 us);
 //  - larger frames: one-wave workgroups, at most kF32CapWavesPerCU resident
-//    per CU (12 up to 32 sets per CU).  8192^2: 58.6-58.7 us at 9-10 waves/CU
+//    per CU (12 up to 32 sets per CU).  Round 3, before the per-position
+//    quantiser and the cap of 7: 8192^2: 58.6-58.7 us at 9-10 waves/CU
 //    against 61.8-62.1 for the uncapped 512-thread kernel and 62.5 for the
 //    uncapped one-wave kernel; 16384^2: 218-219 against 238; 2048 x 16384:
 //    33.7 against 35.0 (profiles/r03/m/kb3_occsz_*.log).  With the cap the

@@ -71,8 +71,11 @@ constexpr int kRtWaves = kRecon == kRtReconF32 ? 2 : 4;
 // against 79.7 us; per-wave atomics 607 us.
 // kQMode: 0 IEEE division (kFast false), 1 the verified 3-op quotient (kFast),
 // 2 as 1 with the default JPEG table's per-position 3-op forms (kVarJpegQ).
-// kBlock: threads per workgroup (512 in the product; A/B in tools/kbench3 "jqrt")
-template <int kRecon, bool kStats, int kQMode, int kRaw = 2, bool kStraddle = false, int kBlock = 512>
+// kBlock: threads per workgroup.  256 since round 4 (8192^2, u8 recon: 77.9-78.3
+// against 78.6-80.7 us with sums, 68.8 against 70.8 without, 1024: 87.0;
+// profiles/r04/b/kb3_jqrtb_8192.log)
+constexpr int kRtBlock = 256;
+template <int kRecon, bool kStats, int kQMode, int kRaw = 2, bool kStraddle = false, int kBlock = kRtBlock>
 __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(const uint8_t* __restrict__ img,
                                                                           float* __restrict__ coef,
                                                                           void* __restrict__ recon,
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
     }
 }
 
-inline dim3 roundtrip_grid(const TileGrid& g, uint32_t block = 512) {
+inline dim3 roundtrip_grid(const TileGrid& g, uint32_t block = kRtBlock) {
     const uint32_t sets = (g.ntiles + 63u) / 64u, waves = block / 64u;
     return dim3((sets + waves - 1u) / waves);
 }
@@ -229,13 +232,13 @@ hipError_t go(const uint8_t* img, float* coef, void* recon, RtSums* sums, const 
               hipStream_t s) {
     if constexpr (kQMode != 0) {
         if (g.tiles_x % 64u != 0u) {  // straddling sets: two-run staged stores (kVarStraddle)
-            hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode, 2, true>), roundtrip_grid(g), dim3(512), 0,
-                               s, img, coef, recon, sums, g, qp);
+            hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode, 2, true>), roundtrip_grid(g), dim3(kRtBlock),
+                               0, s, img, coef, recon, sums, g, qp);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode>), roundtrip_grid(g), dim3(512), 0, s, img, coef,
-                       recon, sums, g, qp);
+    hipLaunchKernelGGL((roundtrip_kernel<kRecon, kStats, kQMode>), roundtrip_grid(g), dim3(kRtBlock), 0, s, img,
+                       coef, recon, sums, g, qp);
     return hipGetLastError();
 }
 template <int kRecon, bool kStats>

@@ -50,6 +50,8 @@ void persist(const int8_t* in, float* out, uint64_t n, hipStream_t s) {
                        in, out, n);
 }
 
+void product(const int8_t* in, float* out, uint64_t n, hipStream_t s) { (void)launch_decode_i8_f32(in, out, n, s); }
+
 struct V {
     const char* name;
     Fn fn;
@@ -61,18 +63,23 @@ int main(int argc, char** argv) {
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;
     const int nsets = std::max<int>(2, (int)((4ull << 28) / n + ((4ull << 28) % n != 0)));
     std::vector<V> vars = {
-        {"b256 1 KiB/wave (product)", one_shot<256, 1>},
+        {"b256 1 KiB/wave (round-4 first)", one_shot<256, 1>},
+        {"product (hpdct_decode_i8_f32 launcher)", product},
         {"b256 2 KiB/wave", one_shot<256, 2>},
         {"b256 4 KiB/wave", one_shot<256, 4>},
         {"b512 1 KiB/wave", one_shot<512, 1>},
         {"b64 1 KiB cap 8 w/cu", capped<1, 8>},
+        {"b64 1 KiB cap 10 w/cu", capped<1, 10>},
         {"b64 1 KiB cap 12 w/cu", capped<1, 12>},
+        {"b64 1 KiB cap 14 w/cu", capped<1, 14>},
+        {"b64 1 KiB cap 16 w/cu", capped<1, 16>},
+        {"b64 1 KiB cap 12 w/cu again", capped<1, 12>},
         {"b64 2 KiB cap 8 w/cu", capped<2, 8>},
         {"b64 2 KiB cap 16 w/cu", capped<2, 16>},
         {"b256 1 KiB persistent 8 w/cu", persist<256, 1, 8>},
         {"b256 1 KiB persistent 16 w/cu", persist<256, 1, 16>},
         {"b256 2 KiB persistent 16 w/cu", persist<256, 2, 16>},
-        {"b256 1 KiB/wave (product) again", one_shot<256, 1>},
+        {"product again", product},
     };
     std::vector<int8_t*> in(nsets);
     std::vector<float*> out(nsets);

@@ -201,7 +201,7 @@ void rt_fused(const void* in, void* out, const Ctx& c, hipStream_t s) {
 template <int kRaw, bool kMemset = true>
 void rt_raw(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kMemset) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, true, kRaw, false, 512>), roundtrip_grid(c.g, 512), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef2[set_of(in)], out, g_sums, c.g, c.qp);
 }
 

@@ -100,13 +100,13 @@ int set_of(const void* in) {
 template <bool kStats>
 void rt_prod(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, true, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, true, 2, false, 512>), roundtrip_grid(c.g, 512), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
 }
 template <bool kStats>
 void rt_pk(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((rtpk::roundtrip_pk_kernel<kStats>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((rtpk::roundtrip_pk_kernel<kStats>), roundtrip_grid(c.g, 512), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], static_cast<uint8_t*>(out),
                        kStats ? g_sums : nullptr, c.g, c.qp);
 }
@@ -264,14 +264,14 @@ void prod_i8_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
 template <bool kStats, int kQMode>
 void rt_q(const void* in, void* out, const Ctx& c, hipStream_t s) {
     if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false, 512>), roundtrip_grid(c.g, 512), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g, c.qp);
 }
 // the sums zeroed by three stream write-value commands instead of a memset
 template <int kQMode>
 void rt_wv(const void* in, void* out, const Ctx& c, hipStream_t s) {
     for (int k = 0; k < 3; ++k) (void)hipStreamWriteValue64(s, reinterpret_cast<uint64_t*>(g_sums) + k, 0ull, 0);
-    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, kQMode, 2, false>), roundtrip_grid(c.g), dim3(512), 0, s,
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, kQMode, 2, false, 512>), roundtrip_grid(c.g, 512), dim3(512), 0, s,
                        static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, g_sums, c.g, c.qp);
 }
 template <bool kStats, int kQMode, int kB>
@@ -284,10 +284,10 @@ void rt_qb(const void* in, void* out, const Ctx& c, hipStream_t s) {
 // C3 round trip (512-thread workgroups), capped at kWg workgroups per CU (0: uncapped)
 template <bool kStats, uint32_t kWg>
 void rt_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    auto* k = roundtrip_kernel<kRtReconU8, kStats, true, 2, false>;
+    auto* k = roundtrip_kernel<kRtReconU8, kStats, true, 2, false, 512>;
     static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
     if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL(k, roundtrip_grid(c.g), dim3(512), dyn, s, static_cast<const uint8_t*>(in), g_coef[set_of(in)],
+    hipLaunchKernelGGL(k, roundtrip_grid(c.g, 512), dim3(512), dyn, s, static_cast<const uint8_t*>(in), g_coef[set_of(in)],
                        out, kStats ? g_sums : nullptr, c.g, c.qp);
 }
 // fp32 inverse (duo mapping, built-in T, dequantise), coefficients from g_coef, capped (0: uncapped)
@@ -537,6 +537,14 @@ int main(int argc, char** argv) {
         {"jqcap", "fwd u8->f32 jpegq cap 7 w/cu b", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
         {"jqcap", "fwd u8->f32 jpegq cap 10 w/cu c", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
         {"jqcap", "fwd u8->f32 jpegq cap 7 w/cu c", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        // round 4, session 4: the cap per frame size with the JPEG forms (run at 16384^2, 2048x16384, 4096^2)
+        {"capsz", "fwd u8->f32 jpegq cap 7 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq cap 8 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 8>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq cap 12 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 12>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq scalar b1024 uncapped", prod_f32_fwd<(P & ~(3u << 12)) | (3u << 12) | kVarJpegQ>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq cap 7 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
+        {"capsz", "fwd u8->f32 jpegq cap 12 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 12>, 5, 4, true},
         // round trip workgroup size
         {"jqrtb", "rt + sums, jpegq b512", rt_q<true, 2>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b256", rt_qb<true, 2, 256>, 6, 1, true},
