@@ -136,17 +136,24 @@ hipError_t fdct_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g,
 
 // uint8 -> fp32 tile kernels (the headline):
 //  - frames of at most kBigWgSetsPerCU sets per CU, where the whole grid is
-//    about one round of resident waves: 1024-thread workgroups, no cap (4096^2:
-//    15.8 us against 17.9-18.8 capped; round 2: 2048 x 16384 35.2 -> 32.3 us);
+//    one or two rounds of resident waves: 1024-thread workgroups, no cap
+//    (4096^2: 16.3 us against 18.2-20.0 capped at 7-12; 2048 x 16384 (32 sets
+//    per CU, the C4 8-way slab): 32.6 against 33.3-34.5 capped at 7-12 --
+//    round 4, profiles/r04/c/kb3_capsz_*.log; round 3 had capped 17-32 sets
+//    per CU at 12 per CU);
 //  - larger frames: one-wave workgroups, at most kF32CapWavesPerCU resident
-//    per CU (12 up to 32 sets per CU).  Round 3, before the per-position
+//    per CU (16384^2: 214.8-215.6 us at 7, 219-220 at 8-10, 222 at 12,
+//    250 uncapped 1024-thread).  Round 3, before the per-position
 //    quantiser and the cap of 7: 8192^2: 58.6-58.7 us at 9-10 waves/CU
 //    against 61.8-62.1 for the uncapped 512-thread kernel and 62.5 for the
 //    uncapped one-wave kernel; 16384^2: 218-219 against 238; 2048 x 16384:
 //    33.7 against 35.0 (profiles/r03/m/kb3_occsz_*.log).  With the cap the
 //    packed-fp32 transform (kVarPacked) gains another 1-2 % (8192^2: 57.6 at
 //    10 waves/CU against 58.7 for the scalar form).
-constexpr uint32_t kBigWgSetsPerCU = 16;
+constexpr uint32_t kBigWgSetsPerCU = 32;
+// frame lists (fdct_frames_go) keep round 3's tiers: uncapped 512-thread
+// workgroups up to 16 sets per CU, capped at 12 waves per CU up to 32
+constexpr uint32_t kFramesUncappedSetsPerCU = 16;
 constexpr uint32_t kMidCapSetsPerCU = 32;
 constexpr uint32_t kF32CapWavesPerCUMid = 12;
 constexpr unsigned kOneWaveWg = 1u << 12;
@@ -160,8 +167,7 @@ hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGri
             return fdct_go<(kV & ~(3u << 12)) | (3u << 12), TIn, TOut, kQuant, kBuiltinT, kWriteback>(
                 img, out, shifted, g, t_dev, q, shift, s);
         return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg | kVarPacked, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
-            img, out, shifted, g, t_dev, q, shift, s,
-            sets_per_cu <= kMidCapSetsPerCU ? kF32CapWavesPerCUMid : kF32CapWavesPerCU);
+            img, out, shifted, g, t_dev, q, shift, s, kF32CapWavesPerCU);
     }
     return fdct_go<kV, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
 }
@@ -402,7 +408,7 @@ hipError_t fdct_frames_go(const FrameTable<TOut>& ft, int n, const TileGrid& g, 
         // the headline's residency cap when the whole list is a large grid
         const uint64_t sets = static_cast<uint64_t>((g.ntiles + 63u) / 64u) * static_cast<uint64_t>(n);
         const uint64_t per_cu = (sets + device_cus() - 1u) / device_cus();
-        if (per_cu > kBigWgSetsPerCU) {
+        if (per_cu > kFramesUncappedSetsPerCU) {
             constexpr unsigned kC = (kV & ~(3u << 12)) | kOneWaveWg | kVarPacked;
             auto* kern = fdct_frames_kernel<TOut, kC>;
             static const size_t st = static_lds_of(kern);

@@ -496,15 +496,17 @@ def test_video_widths_large_frames(hp, oracle, dev, h, w):
     assert sums["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
 
 
-@pytest.mark.parametrize("h,w", [(4104, 8200), (3000, 8008), (2048, 16384)])
+@pytest.mark.parametrize("h,w", [(4104, 8200), (6000, 8008), (2048, 16384)])
 @pytest.mark.parametrize("qtab", ["jpeg", "fractional"])
 def test_capped_packed_forward_large_frames(hp, oracle, dev, h, w, qtab):
-    """u8 -> fp32 frames of more than 16 sets per CU take the one-wave,
-    residency-capped, packed-fp32 kernel (hpdct_launch.hpp fdct_tile_go):
-    cap 10 above 32 sets per CU (4104 x 8200), cap 12 up to 32 (3000 x 8008,
-    2048 x 16384).  Ragged widths (tiles_x not a multiple of 64: sets straddle
-    tile rows) and a ragged last set; the JPEG table (3-op quotient per half)
-    and a fractional table (IEEE division per half).  Bit-exact vs the oracle."""
+    """u8 -> fp32 frames of more than 32 sets per CU take the one-wave,
+    residency-capped (7 per CU), packed-fp32 kernel (hpdct_launch.hpp
+    fdct_tile_go): 4104 x 8200 (32.1 sets per CU), 6000 x 8008 (45.8); frames
+    of up to 32 take the uncapped 1024-thread kernel: 2048 x 16384 (the C4
+    8-way slab, exactly 32).  Ragged widths (tiles_x not a multiple of 64:
+    sets straddle tile rows) and a ragged last set; the JPEG table (per-position
+    forms, 3-op quotient elsewhere) and a fractional table (IEEE division per
+    half).  Bit-exact vs the oracle."""
     img = oracle.hash_u8(h * w, seed=h + w).reshape(h, w)
     Q = None
     if qtab == "fractional":
@@ -589,8 +591,8 @@ def test_quantiser_hardest_tiles(hp, dev, hardest):
     assert bits_equal(to_host(hp.forward(x)), ref), mismatches(to_host(hp.forward(x)), ref)
     got8 = to_host(hp.forward(x, out_dtype=torch.int8))
     assert np.array_equal(got8.astype(np.float32), ref)
-    # the same tiles in a frame large enough for the capped packed kernel (> 16 sets per CU)
-    h = 8 * (-(-(17 * 256 * 64 * 64) // img.size))
+    # the same tiles in a frame large enough for the capped packed kernel (> 32 sets per CU)
+    h = 8 * (-(-(33 * 256 * 64 * 64) // img.size))
     big = np.ascontiguousarray(np.tile(img, (h // 8, 1)))
     refb = np.tile(ref, (h // 8, 1))
     xb = to_dev(big, dev)
