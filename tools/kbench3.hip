@@ -545,6 +545,22 @@ int main(int argc, char** argv) {
         {"capsz", "fwd u8->f32 jpegq scalar b1024 uncapped", prod_f32_fwd<(P & ~(3u << 12)) | (3u << 12) | kVarJpegQ>, 5, 4, true},
         {"capsz", "fwd u8->f32 jpegq cap 7 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 7>, 5, 4, true},
         {"capsz", "fwd u8->f32 jpegq cap 12 w/cu again", prod_f32_fwd_cap<PK1 | kVarJpegQ, 12>, 5, 4, true},
+        // round 4, session 5: the fp32 duo inverse's cap below 10 (the headline moved from 10 to 7)
+        {"invc", "inv f32->f32 duo b64 cap 10 w/cu (product)", inv_cap_v<kDuoVar | (1u << 12), 10>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 6 w/cu", inv_cap_v<kDuoVar | (1u << 12), 6>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 7 w/cu", inv_cap_v<kDuoVar | (1u << 12), 7>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 8 w/cu", inv_cap_v<kDuoVar | (1u << 12), 8>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 10 w/cu again", inv_cap_v<kDuoVar | (1u << 12), 10>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 7 w/cu again", inv_cap_v<kDuoVar | (1u << 12), 7>, 8, 4, true},
+        {"invc", "inv f32->f32 duo b64 cap 8 w/cu again", inv_cap_v<kDuoVar | (1u << 12), 8>, 8, 4, true},
+        // int8 forward, one-wave workgroups at higher caps (VALU-bound: needs waves)
+        {"i8cap", "fwd u8->i8 jpegq b256 (product)", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b64 cap 16 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 16>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b64 cap 20 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 20>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b64 cap 24 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 24>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b256 cap 24 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | kVarJpegQ, 6>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b256 (product) again", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
+        {"i8cap", "fwd u8->i8 jpegq b64 cap 20 w/cu again", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 20>, 2, 1, true},
         // round trip workgroup size
         {"jqrtb", "rt + sums, jpegq b512", rt_q<true, 2>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b256", rt_qb<true, 2, 256>, 6, 1, true},
@@ -599,7 +615,7 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb";
+               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc";
     });
     if (want_coef) {
         g_img = img;
