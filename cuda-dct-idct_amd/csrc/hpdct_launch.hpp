@@ -91,7 +91,8 @@ size_t static_lds_of(K kern) {
 // legal.  512-thread workgroups (1-3 % faster than 256 on every kernel in
 // round 1), except the int8 output: 256-thread workgroups since its JPEG-form
 // quantiser (round 4: 8192^2 28.9 against 29.8-30.0 us with 512,
-// profiles/r04/a/kb3_jqi8_8192.log).
+// profiles/r04/a/kb3_jqi8_8192.log), and with the JPEG forms one-wave
+// workgroups under a residency cap (fdct_tile_go, kI8CapWavesPerCU).
 template <typename TIn, typename TOut>
 constexpr unsigned kProdVar = (std::is_same_v<TOut, int8_t> ? 0u : (2u << 12)) | kVarNT |
                               (std::is_same_v<TOut, float> ? kVarLdsStore : 0u) |
@@ -157,6 +158,12 @@ constexpr uint32_t kFramesUncappedSetsPerCU = 16;
 constexpr uint32_t kMidCapSetsPerCU = 32;
 constexpr uint32_t kF32CapWavesPerCUMid = 12;
 constexpr unsigned kOneWaveWg = 1u << 12;
+// uint8 -> int8 with the default JPEG table's forms: one-wave workgroups, at
+// most kI8CapWavesPerCU resident per CU (round 4, two boxes: 8192^2
+// 29.6-31.1 against 30.8-32.6 us for 256-thread workgroups, 4096^2 9.1-9.2
+// against 9.5-9.6, 16384^2 equal; 24 per CU: 30.0-32.2.
+// profiles/r04/f/kb3_i8cap_*.log, profiles/r04/g/kb3_i8cap_*.log)
+constexpr uint32_t kI8CapWavesPerCU = 20;
 
 template <unsigned kV, typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
@@ -168,6 +175,10 @@ hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGri
                 img, out, shifted, g, t_dev, q, shift, s);
         return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg | kVarPacked, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
             img, out, shifted, g, t_dev, q, shift, s, kF32CapWavesPerCU);
+    }
+    if constexpr (std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, int8_t> && (kV & kVarJpegQ) != 0u) {
+        return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
+            img, out, shifted, g, t_dev, q, shift, s, kI8CapWavesPerCU);
     }
     return fdct_go<kV, TIn, TOut, kQuant, kBuiltinT, kWriteback>(img, out, shifted, g, t_dev, q, shift, s);
 }

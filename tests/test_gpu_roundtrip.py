@@ -126,6 +126,40 @@ def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
         check_sums(hp.sums_from_buffer(buf), want)
 
 
+def test_roundtrip_in_a_hip_graph(hp, oracle, dev):
+    """hpdct_roundtrip_u8 captured into a HIP graph (its sums memset and the
+    kernel) next to an accumulate launch: every replay overwrites the one-pass
+    sums with the frame's totals and adds the other frame's into the ring slot
+    once more; coefficients are the frame's each time."""
+    import torch
+    a = oracle.rand_u8(64 * 128, 31).reshape(64, 128)
+    b = oracle.rand_u8(72 * 256, 32).reshape(72, 256)
+    qa, _, _, want_a = expected(oracle, a)
+    want_b = expected(oracle, b)[3]
+    xa, xb = to_dev(a, dev), to_dev(b, dev)
+    ca = torch.empty(xa.shape, dtype=torch.float32, device=dev)
+    cb = torch.empty(xb.shape, dtype=torch.float32, device=dev)
+    sums = torch.full((3,), -9, dtype=torch.int64, device=dev)
+    ring = torch.zeros(3, dtype=torch.int64, device=dev)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g):
+            hp.bind_roundtrip(xa, ca, None, sums)()
+            hp.bind_roundtrip(xb, cb, None, ring, accumulate=True)()
+    torch.cuda.synchronize()
+    for k in range(1, 4):
+        sums.fill_(-1)
+        ca.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        check_sums(hp.sums_from_buffer(sums), want_a)
+        assert bits_equal(to_host(ca), qa)
+        got = hp.sums_from_buffer(ring)
+        assert got["sum_x2"] == k * want_b["sum_x2"] and got["sse_u8"] == k * want_b["sse_u8"]
+
+
 def test_roundtrip_accumulate_adds_into_caller_zeroed_sums(hp, oracle, dev):
     """hpdct_roundtrip_u8_accumulate: no memset; each frame's sums are added to
     the caller's struct.  A zeroed ring of per-frame slots gives the per-frame
