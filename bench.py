@@ -483,8 +483,8 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         qd = hpdct.quality_from_sums(hpdct.sums_from_buffer(sums_buf), px)
         one_ms = rms1 / steps
         # the same with a caller-zeroed ring of per-frame sums slots
-        # (hpdct_roundtrip_u8_accumulate: no 24-byte memset kernel per launch;
-        # one memset zeroes the ring before the loop)
+        # (hpdct_roundtrip_u8_accumulate: one kernel per launch, no sums
+        # finish kernel; one memset zeroes the ring before the loop)
         ring_n = 1024
         ring = torch.zeros((ring_n, 3), dtype=torch.int64, device=dev)
         acc = [hpdct.bind_roundtrip(imgs[i % args.sets], outs[i % args.sets], rt_px[i % 2], ring[i], stream=stream,
@@ -501,8 +501,9 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                             "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
             "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums", n),
                              quality_from_device_sums=qd,
-                             note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums, one "
-                                  "kernel; bit-identical to the two kernels"),
+                             note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums in one "
+                                  "pass (the round trip + a one-wave kernel that moves the sums from the library's "
+                                  "slot over the caller's struct); bit-identical to the two kernels"),
             "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
                                        note="hpdct_roundtrip_u8_accumulate into a caller-zeroed ring of 1024 "
                                             "per-frame sums slots; the ring's one memset per 1024 frames is "

@@ -57,8 +57,10 @@ struct RtSums {
 enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
 // fast: integer table in 1..255 with int8-range quotients (verified quotient,
 // packed int8 rows); sums may be nullptr (no statistics), recon nullptr with
-// kRtReconNone.  Zeroes *sums on the stream before the kernel.
-// zero_sums: hipMemsetAsync the sums before the kernel (else they accumulate)
+// kRtReconNone.
+// zero_sums: the launch overwrites *sums (the kernel adds into a library slot
+// kept per sums pointer, a one-wave kernel moves it over *sums; a memset of
+// *sums before the kernel when no slot can be had); false: adds into *sums
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s);
 

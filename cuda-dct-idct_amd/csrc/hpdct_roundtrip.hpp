@@ -23,7 +23,10 @@
 //             result does not depend on the order tiles finish in, but it is
 //             not the exact sum (each tile's fp32 chain rounds; relative error
 //             ~1e-9 at 8192^2, tests/test_gpu_roundtrip.py)
-// Workgroup partials are added with one 64-bit atomic per field per workgroup.
+// Workgroup partials are added with one 64-bit atomic per field per workgroup,
+// into the caller's struct (hpdct_roundtrip_u8_accumulate) or into a library
+// slot that rt_finish_kernel then copies over the caller's struct and zeroes
+// (hpdct_roundtrip_u8).
 #pragma once
 
 #include "hpdct_kernels_impl.hpp"
@@ -221,6 +224,19 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
     }
 }
 
+// hpdct_roundtrip_u8's sums: the round trip adds into a library slot (all
+// zero between launches); this one-wave kernel, next on the stream, writes
+// the slot over the caller's struct and zeroes it.  8192^2: 77.6 us per
+// launch against 79.3 with a memset of the caller's struct before the kernel
+// and 76.6 with no zeroing at all (profiles/r04/j/kb3_rtring_8192.log).
+__global__ __launch_bounds__(64) void rt_finish_kernel(RtSums* __restrict__ dst, RtSums* __restrict__ slot) {
+    if (threadIdx.x < 3u) {
+        unsigned long long* const src = reinterpret_cast<unsigned long long*>(slot) + threadIdx.x;
+        reinterpret_cast<unsigned long long*>(dst)[threadIdx.x] = *src;
+        *src = 0ull;
+    }
+}
+
 inline dim3 roundtrip_grid(const TileGrid& g, uint32_t block = kRtBlock) {
     const uint32_t sets = (g.ntiles + 63u) / 64u, waves = block / 64u;
     return dim3((sets + waves - 1u) / waves);
@@ -259,19 +275,28 @@ hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, cons
 }  // namespace rt_detail
 
 // fast: 0 IEEE division, 1 the verified 3-op quotient, 2 with the default
-// JPEG table's per-position forms (hpdct_kernels.h launch_roundtrip)
+// JPEG table's per-position forms (hpdct_kernels.h launch_roundtrip).
+// Sums: zero_sums false adds into *sums; else with a slot (all zero, kept for
+// this sums pointer by the caller of this function) the kernel adds into the
+// slot and rt_finish_kernel moves it over *sums, and without one a memset
+// zeroes *sums before the kernel.
 inline hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
                                         RtSums* sums, const TileGrid& g, const QParams& qp, int fast,
-                                        hipStream_t s, bool zero_sums = true) {
-    if (sums && zero_sums) {
+                                        hipStream_t s, bool zero_sums = true, RtSums* slot = nullptr) {
+    RtSums* const acc = sums && zero_sums && slot ? slot : sums;
+    if (sums && zero_sums && !slot) {
         const hipError_t e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);
         if (e != hipSuccess) return e;
     }
+    hipError_t e;
     switch (recon_kind) {
-        case kRtReconU8: return rt_detail::go_r<kRtReconU8>(img, coef, recon, sums, g, qp, fast, s);
-        case kRtReconF32: return rt_detail::go_r<kRtReconF32>(img, coef, recon, sums, g, qp, fast, s);
-        default: return rt_detail::go_r<kRtReconNone>(img, coef, nullptr, sums, g, qp, fast, s);
+        case kRtReconU8: e = rt_detail::go_r<kRtReconU8>(img, coef, recon, acc, g, qp, fast, s); break;
+        case kRtReconF32: e = rt_detail::go_r<kRtReconF32>(img, coef, recon, acc, g, qp, fast, s); break;
+        default: e = rt_detail::go_r<kRtReconNone>(img, coef, nullptr, acc, g, qp, fast, s); break;
     }
+    if (e != hipSuccess || acc == sums) return e;
+    hipLaunchKernelGGL(rt_finish_kernel, dim3(1), dim3(64), 0, s, sums, slot);
+    return hipGetLastError();
 }
 
 }  // namespace hpdct

@@ -103,10 +103,11 @@ def test_roundtrip_sums_only_and_no_sums(hp, oracle, dev):
 
 
 def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
-    """The sums are written (not accumulated) by each launch: the library
-    zeroes the struct on the launch stream before the kernel, so back-to-back
-    launches of different grid sizes, a garbage-filled sums buffer, and
-    launches on a second stream all give this frame's totals."""
+    """The sums are written (not accumulated) by each launch: the kernel adds
+    into the library's slot for the sums pointer and a one-wave kernel moves
+    it over the struct, so back-to-back launches of different grid sizes, a
+    garbage-filled sums buffer, and launches on a second stream all give this
+    frame's totals."""
     import torch
     a = oracle.rand_u8(64 * 128, 11).reshape(64, 128)
     b = oracle.rand_u8(520 * 1008, 12).reshape(520, 1008)
@@ -127,10 +128,12 @@ def test_roundtrip_sums_repeat_and_streams(hp, oracle, dev):
 
 
 def test_roundtrip_in_a_hip_graph(hp, oracle, dev):
-    """hpdct_roundtrip_u8 captured into a HIP graph (its sums memset and the
-    kernel) next to an accumulate launch: every replay overwrites the one-pass
-    sums with the frame's totals and adds the other frame's into the ring slot
-    once more; coefficients are the frame's each time."""
+    """hpdct_roundtrip_u8 captured into a HIP graph (the round trip and the
+    sums finish kernel, or the memset fallback when the sums pointer is new
+    and its slot would need an allocation inside the capture) next to an
+    accumulate launch: every replay overwrites the one-pass sums with the
+    frame's totals and adds the other frame's into the ring slot once more;
+    coefficients are the frame's each time."""
     import torch
     a = oracle.rand_u8(64 * 128, 31).reshape(64, 128)
     b = oracle.rand_u8(72 * 256, 32).reshape(72, 256)
@@ -160,8 +163,45 @@ def test_roundtrip_in_a_hip_graph(hp, oracle, dev):
         assert got["sum_x2"] == k * want_b["sum_x2"] and got["sse_u8"] == k * want_b["sse_u8"]
 
 
+def test_roundtrip_sums_slots_many_buffers(hp, oracle, dev):
+    """hpdct_roundtrip_u8's sums slots (hpdct_roundtrip.hip): one per sums
+    pointer, handed out from zeroed 1024-slot chunks and left zero by every
+    launch.  1100 distinct sums buffers (more than one chunk) each get the
+    frame's totals, then another frame's on reuse; an accumulate launch on a
+    slotted buffer adds into the buffer itself and leaves the slot alone."""
+    import torch
+    a = oracle.rand_u8(64 * 128, 41).reshape(64, 128)
+    b = oracle.rand_u8(72 * 256, 42).reshape(72, 256)
+    want_a, want_b = expected(oracle, a)[3], expected(oracle, b)[3]
+    xa, xb = to_dev(a, dev), to_dev(b, dev)
+    ca = torch.empty(xa.shape, dtype=torch.float32, device=dev)
+    cb = torch.empty(xb.shape, dtype=torch.float32, device=dev)
+
+    def all_rows(buf, want):
+        rows = buf.cpu()
+        assert torch.equal(rows, rows[:1].expand_as(rows))
+        check_sums(hp.sums_from_buffer(rows[0]), want)
+
+    many = torch.full((1100, 3), -7, dtype=torch.int64, device=dev)
+    for i in range(many.shape[0]):
+        hp.bind_roundtrip(xa, ca, None, many[i])()
+    torch.cuda.synchronize()
+    all_rows(many, want_a)
+    for i in range(many.shape[0]):
+        hp.bind_roundtrip(xb, cb, None, many[i])()
+    torch.cuda.synchronize()
+    all_rows(many, want_b)
+    hp.bind_roundtrip(xa, ca, None, many[5], accumulate=True)()
+    torch.cuda.synchronize()
+    s5 = hp.sums_from_buffer(many[5])
+    assert s5["sum_x2"] == want_a["sum_x2"] + want_b["sum_x2"] and s5["sse_u8"] == want_a["sse_u8"] + want_b["sse_u8"]
+    hp.bind_roundtrip(xa, ca, None, many[5])()
+    torch.cuda.synchronize()
+    check_sums(hp.sums_from_buffer(many[5]), want_a)
+
+
 def test_roundtrip_accumulate_adds_into_caller_zeroed_sums(hp, oracle, dev):
-    """hpdct_roundtrip_u8_accumulate: no memset; each frame's sums are added to
+    """hpdct_roundtrip_u8_accumulate: one kernel; each frame's sums are added to
     the caller's struct.  A zeroed ring of per-frame slots gives the per-frame
     totals; two frames sharing a slot give the sum of both (exact integer
     fields, sse_f32 to the fixed-point unit); coefficients and reconstruction

@@ -92,6 +92,9 @@ std::vector<uint8_t*> g_img;
 std::vector<float*> g_coef;
 std::vector<float*> g_shift;  // drop-in forward's X-128 write-back planes
 RtSums* g_sums = nullptr;
+RtSums* g_sums_ring = nullptr;  // kRing slots: each launch adds into the next one
+constexpr int kRing = 1024;
+int g_ring_next = 0;
 int set_of(const void* in) {
     for (size_t i = 0; i < g_img.size(); ++i)
         if (g_img[i] == in) return (int)i;
@@ -280,6 +283,30 @@ void rt_qb(const void* in, void* out, const Ctx& c, hipStream_t s) {
     hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, kQMode, 2, false, kB>), roundtrip_grid(c.g, kB), dim3(kB),
                        0, s, static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, kStats ? g_sums : nullptr, c.g,
                        c.qp);
+}
+// one wave: the caller's sums = the slot's, and the slot back to zero
+__global__ __launch_bounds__(64) void rt_finish_probe(RtSums* __restrict__ dst, RtSums* __restrict__ slot) {
+    if (threadIdx.x < 3u) {
+        auto* const src = reinterpret_cast<unsigned long long*>(slot) + threadIdx.x;
+        reinterpret_cast<unsigned long long*>(dst)[threadIdx.x] = *src;
+        *src = 0ull;
+    }
+}
+// C3 round trip, 256-thread workgroups, where the sums go: kMode 0 the same
+// struct every launch (hpdct_roundtrip_u8_accumulate into one struct), 1 the
+// next slot of a ring (the driver bench's sums ring), 2 ring slot + a 24-byte
+// device copy into the one struct after the kernel, 3 memset of the one struct
+// + kernel (hpdct_roundtrip_u8), 4 memset of the ring slot + kernel, 5 one
+// library slot + a one-wave kernel that copies it out and zeroes it
+template <int kMode>
+void rt_where(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    RtSums* const slot = g_sums_ring + (g_ring_next++ % (kRing - 1));  // kRing - 1: mode 5's slot
+    RtSums* const dst = kMode == 0 || kMode == 3 ? g_sums : kMode == 5 ? g_sums_ring + kRing - 1 : slot;
+    if (kMode == 3 || kMode == 4) (void)hipMemsetAsync(dst, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, true, 2, 2, false, 256>), roundtrip_grid(c.g, 256), dim3(256), 0,
+                       s, static_cast<const uint8_t*>(in), g_coef[set_of(in)], out, dst, c.g, c.qp);
+    if (kMode == 2) (void)hipMemcpyAsync(g_sums, slot, sizeof(RtSums), hipMemcpyDeviceToDevice, s);
+    if (kMode == 5) hipLaunchKernelGGL(rt_finish_probe, dim3(1), dim3(64), 0, s, g_sums, dst);
 }
 // C3 round trip (512-thread workgroups), capped at kWg workgroups per CU (0: uncapped)
 template <bool kStats, uint32_t kWg>
@@ -571,6 +598,19 @@ int main(int argc, char** argv) {
         {"jqrtb", "rt + sums, jpegq b256 again", rt_qb<true, 2, 256>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq, zeroed by write-value", rt_wv<2>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b512 again 2", rt_q<true, 2>, 6, 1, true},
+        // round trip: which cache line the sums go to, memset or not
+        {"rtring", "rt sums: one struct, accumulate", rt_where<0>, 6, 1, true},
+        {"rtring", "rt sums: ring slot, accumulate", rt_where<1>, 6, 1, true},
+        {"rtring", "rt sums: ring slot + 24 B copy", rt_where<2>, 6, 1, true},
+        {"rtring", "rt sums: memset one struct (product)", rt_where<3>, 6, 1, true},
+        {"rtring", "rt sums: memset ring slot", rt_where<4>, 6, 1, true},
+        {"rtring", "rt no sums", rt_qb<false, 2, 256>, 6, 1, true},
+        {"rtring", "rt sums: slot + finish kernel", rt_where<5>, 6, 1, true},
+        {"rtring", "rt sums: one struct, accumulate again", rt_where<0>, 6, 1, true},
+        {"rtring", "rt sums: ring slot, accumulate again", rt_where<1>, 6, 1, true},
+        {"rtring", "rt sums: memset one struct again", rt_where<3>, 6, 1, true},
+        {"rtring", "rt sums: ring slot + 24 B copy again", rt_where<2>, 6, 1, true},
+        {"rtring", "rt sums: slot + finish kernel again", rt_where<5>, 6, 1, true},
         // the headline cap below 8 with the JPEG forms (fewer VALU per set)
         {"jqf", "fwd u8->f32 jpegq cap 10 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 10>, 5, 4, true},
         {"jqf", "fwd u8->f32 jpegq cap 6 w/cu", prod_f32_fwd_cap<PK1 | kVarJpegQ, 6>, 5, 4, true},
@@ -615,7 +655,8 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc";
+               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc" ||
+               v.group == "rtring";
     });
     if (want_coef) {
         g_img = img;
@@ -626,6 +667,8 @@ int main(int argc, char** argv) {
             for (auto& p : g_shift) CK(hipMalloc(&p, px * 4));
         }
         CK(hipMalloc(&g_sums, sizeof(RtSums)));
+        CK(hipMalloc(&g_sums_ring, kRing * sizeof(RtSums)));
+        CK(hipMemset(g_sums_ring, 0, kRing * sizeof(RtSums)));
         // the inverse's input: each set's quantised coefficients (the forward of its frame)
         for (int k = 0; k < nsets; ++k) hipLaunchKernelGGL((hpdct::fdct_kernel<uint8_t, float, true, true, false, kProdVar<uint8_t, float> | kVarFastDiv>),
                                                            grid_for(c.g, false, c.cus, 512), dim3(512), 0, 0, img[k], g_coef[k], nullptr, c.g, nullptr, c.qp, 128.0f);
@@ -649,6 +692,25 @@ int main(int argc, char** argv) {
                cok ? "bit-exact" : "MISMATCH", sok ? "identical" : "DIFFER", (unsigned long long)s1.sse_u8,
                (unsigned long long)s1.sum_x2, (unsigned long long)s1.sse_f32_fx);
         if (!cok || !sok) return 1;
+    }
+    if (std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtring"; })) {
+        // the finish kernel's sums == memset + atomics, launch after launch, and its slot zero after each
+        for (int rep = 0; rep < 4; ++rep) {
+            RtSums s0, s1, z;
+            rt_where<3>(img[rep & 1], out[2], c, 0);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(&s0, g_sums, sizeof(s0), hipMemcpyDeviceToHost));
+            CK(hipMemset(g_sums, 0xa5, sizeof(RtSums)));
+            rt_where<5>(img[rep & 1], out[2], c, 0);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(&s1, g_sums, sizeof(s1), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&z, g_sums_ring + kRing - 1, sizeof(z), hipMemcpyDeviceToHost));
+            const bool sok = memcmp(&s0, &s1, sizeof(s0)) == 0;
+            const bool zok = (z.sse_f32_fx | z.sse_u8 | z.sum_x2) == 0;
+            printf("check rt finish sums set %d: %s (sse_u8 %llu), slot %s\n", rep & 1, sok ? "identical" : "DIFFER",
+                   (unsigned long long)s1.sse_u8, zok ? "zero" : "NOT ZERO");
+            if (!sok || !zok) return 1;
+        }
     }
     // correctness: each variant against its group's first entry, on sets 0 and 1
     {
