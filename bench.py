@@ -339,8 +339,8 @@ def main():
         c4 = extras.get("c4", {})
         # the north_star row-shard figures (C4, 16384^2 over the ranks), top level
         for key in ("compute_speedup_vs_1gpu", "predicted_compute_speedup_2", "predicted_compute_speedup_4",
-                    "predicted_compute_speedup_8", "one_gpu_full_frame_ms", "gather_ms", "gather_int8_ms",
-                    "decode_int8_ms", "end_to_end_ms", "end_to_end_int8_ms", "sharded_equals_unsharded"):
+                    "predicted_compute_speedup_8", "one_gpu_full_frame_ms", "gather_ms", "gather_decode_int8_ms",
+                    "decode_int8_ms", "int8_wire_equals_fp32", "end_to_end_ms", "end_to_end_int8_ms", "sharded_equals_unsharded"):
             if key in c4:
                 result["c4_" + key] = c4[key]
         if "compute_ms_max_rank" in c4:
@@ -482,35 +482,65 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         one[0]()
         qd = hpdct.quality_from_sums(hpdct.sums_from_buffer(sums_buf), px)
         one_ms = rms1 / steps
+        sums_one = hpdct.sums_from_buffer(sums_buf)
         # the same with a caller-zeroed ring of per-frame sums slots
         # (hpdct_roundtrip_u8_accumulate: one kernel per launch, no sums
-        # finish kernel; one memset zeroes the ring before the loop)
-        ring_n = 1024
+        # finish kernel).  The warm-up accumulates into a ring of its own; the
+        # timed launches go to a fresh zeroed ring, one slot each, so after the
+        # region every slot must hold exactly its frame's sums (ring_sums_exact)
+        ref_sums = []
+        for s in range(args.sets):
+            b = torch.zeros(3, dtype=torch.int64, device=dev)
+            hpdct.bind_roundtrip(imgs[s], outs[s], rt_px[0], b, stream=stream)()
+            ref_sums.append(b)
+        warm_ring = torch.zeros((args.sets, 3), dtype=torch.int64, device=dev)
+        warm = [hpdct.bind_roundtrip(imgs[s], outs[s], rt_px[s % 2], warm_ring[s], stream=stream, accumulate=True)
+                for s in range(args.sets)]
+        ring_n = steps
         ring = torch.zeros((ring_n, 3), dtype=torch.int64, device=dev)
         acc = [hpdct.bind_roundtrip(imgs[i % args.sets], outs[i % args.sets], rt_px[i % 2], ring[i], stream=stream,
                                     accumulate=True) for i in range(ring_n)]
-        rms2, k2, _ = timed_loop(acc, steps, 4)
-        acc_ms = rms2 / steps
-        ring.zero_()
-        acc[0]()
+        i, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < EXTRA_WARM_S or i < 2 * len(warm):
+            warm[i % len(warm)]()
+            i += 1
+            if i % 16 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        barrier()
+        ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev_a.record(stream)
+        for c in acc:
+            c()
+        ev_b.record(stream)
+        torch.cuda.synchronize()
+        acc_ms = ev_a.elapsed_time(ev_b) / ring_n
+        want = torch.stack(ref_sums)[torch.arange(ring_n, device=dev) % args.sets]
+        ring_exact = bool(torch.equal(ring, want))
         qa = hpdct.quality_from_sums(hpdct.sums_from_buffer(ring[0]), px)
+        k2 = np.array([acc_ms])
+        rms2 = acc_ms * steps
+        # the device sums against torch's on the two-kernel output: the integer
+        # fields exactly (double is exact below 2^53)
+        sums_exact = sums_one["sse_u8"] == int(se8) and sums_one["sum_x2"] == int(sx)
         extras["c3_roundtrip"] = {
             "mse_f32": se / px, "peen_f32_pct": 100.0 * (se / sx) ** 0.5,
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
             "two_kernels": {"ms_per_frame": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
                             "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
             "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums", n),
-                             quality_from_device_sums=qd,
+                             quality_from_device_sums=qd, sums_exact_vs_two_kernels=sums_exact,
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums in one "
                                   "pass (the round trip + a one-wave kernel that moves the sums from the library's "
                                   "slot over the caller's struct); bit-identical to the two kernels"),
             "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
-                                       note="hpdct_roundtrip_u8_accumulate into a caller-zeroed ring of 1024 "
-                                            "per-frame sums slots; the ring's one memset per 1024 frames is "
-                                            "outside the timed region (amortised: ~3 ns per frame), and slots "
-                                            "reused by the warm-up accumulate (the timing does not depend on it)"),
+                                       ring_sums_exact=ring_exact,
+                                       note="hpdct_roundtrip_u8_accumulate, one slot per timed launch of a fresh "
+                                            "caller-zeroed ring (its memset outside the timed region); the warm-up "
+                                            "accumulates into a ring of its own; ring_sums_exact: every slot equals "
+                                            "its frame's hpdct_roundtrip_u8 sums"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
-        del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc
+        del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc, warm, warm_ring, ref_sums, want
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024
@@ -522,6 +552,27 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         rms, k, _ = timed_loop(calls, 8 * steps, 10)
         line = _line(c2 * c2, rms / (8 * steps), float(k.mean()), BYTES_PER_PX["u8_f32"], world)
         line["note"] = "cache-resident (40 MB working set < 256 MiB MALL): hbm_frac not meaningful"
+        # the floors of that launch (hpdct_floor_probe): an empty kernel on the
+        # forward's own grid, and the same grid copying the same bytes (1 B
+        # read + 4 B NT write per pixel, no transform); VERDICT r4 item 5
+        floor = {}
+        for name, kind in (("empty_kernel_us", hpdct.PROBE_EMPTY), ("copy_same_bytes_us", hpdct.PROBE_COPY)):
+            pc = [hpdct.bind_floor_probe(kind, c2_in[s], c2_out[s], c2, c2, stream=stream) for s in range(8)]
+            frms, _, _ = timed_loop(pc, 8 * steps, 10)
+            floor[name] = round(frms / (8 * steps) * 1e3, 3)
+        fwd_us = rms / (8 * steps) * 1e3
+        floor["forward_us"] = round(fwd_us, 3)
+        floor["forward_minus_copy_us"] = round(fwd_us - floor["copy_same_bytes_us"], 3)
+        # the mapping A/B the floor asks for when the gap exceeds 1 us: the
+        # tile mapping (256 waves of 64 tiles) against AUTO's octet (2,048 waves)
+        try:
+            hpdct.set_mapping("tile")
+            tc = [hpdct.bind("fwd", c2_in[s], c2_out[s], stream=stream) for s in range(8)]
+            trms, _, _ = timed_loop(tc, 8 * steps, 10)
+            floor["forward_tile_mapping_us"] = round(trms / (8 * steps) * 1e3, 3)
+        finally:
+            hpdct.set_mapping("auto")
+        line["floor"] = floor
         extras["c2_fwd_u8_f32"] = line
         del c2_in, c2_out
         # C2 frames batched: a 1024^2 frame is 256 tile sets, one per CU, so a
@@ -688,10 +739,16 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
                                  (world 1 included): the compute-phase node
                                  speedup k GPUs would give (north_star >= 6x
                                  at 8), measured without k GPUs;
-      gather_ms / gather_int8_ms the gather alone (the root computes its own
-                                 slab in place in the frame, so only peer bytes
-                                 move: 0 at world 1);
-      decode_int8_ms             the root's int8 -> fp32 decode (HIP kernel);
+      gather_ms                  the fp32 gather alone (the root computes its
+                                 own slab in place in the frame, so only peer
+                                 bytes move: 0 at world 1);
+      gather_decode_int8_ms      the int8 wire's gather: peers' int8 slabs to
+                                 the root, decoded there into its fp32 frame
+                                 (peer rows only; the root's own slab is fp32
+                                 in place: nothing at world 1);
+      decode_int8_ms             the root's int8 -> fp32 decode kernel over a
+                                 whole frame, inputs rotated past the Infinity
+                                 Cache (decode_int8_sets frames);
       end_to_end_ms / end_to_end_int8_ms
                                  slab forward + gather (+ decode) between two
                                  barriers, max over ranks: what a caller that
@@ -768,15 +825,21 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     else:
         out["gather_path"] = "none (one process, no process group: the slab is the frame)"
 
-    # root: the frame buffers, its own slab written in place; others: slab buffers
+    # The root's own slab is computed fp32 in place in its frame for BOTH wire
+    # formats: the int8 wire carries only the peers' slabs, which the root
+    # receives into an int8 scratch frame and decodes into the fp32 frame
+    # (hpdct_gather_decode_i8).  Other ranks: slab buffers.
     frame = torch.empty((n, n), dtype=torch.float32, device=dev) if rank == 0 else None
     frame8 = torch.empty((n, n), dtype=torch.int8, device=dev) if rank == 0 else None
     in_place = comm is not None or not use_pg
     if rank == 0 and in_place:
-        y, y8 = frame[r0:r0 + rows], frame8[r0:r0 + rows]
+        y = frame[r0:r0 + rows]
     else:
         y = torch.empty((rows, n), dtype=torch.float32, device=dev)
-        y8 = torch.empty((rows, n), dtype=torch.int8, device=dev)
+    # int8 slab: every rank but a native/one-process root (the gloo rehearsal's
+    # gather takes every rank's slab, the root's own included)
+    y8 = None if (rank == 0 and in_place) else torch.empty((rows, n), dtype=torch.int8, device=dev)
+    own_f32 = frame[r0:r0 + rows] if rank == 0 else None
 
     def forward(dst):
         if comm is not None:
@@ -795,6 +858,30 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
             full.copy_(got)
         return full
 
+    def forward_i8():
+        if rank == 0:
+            forward(own_f32)  # the root's rows: fp32, in place
+            if y8 is not None:
+                forward(y8)
+        else:
+            forward(y8)
+
+    def gather_i8():
+        """peers' int8 slabs -> the root's int8 scratch -> decoded into its fp32
+        frame, peer rows only"""
+        if comm is not None:
+            hpdct.gather_decode_i8(comm, y8 if rank != 0 else None, frame8, frame, n, n, root=0, stream=stream)
+            return
+        if not use_pg:
+            return  # one process: no peers
+        got = gather_slabs(y8, n, n, root=0)
+        if rank == 0:
+            frame8.copy_(got)
+            if r0 > 0:
+                hpdct.decode_i8_f32(frame8[:r0], frame[:r0], stream=stream)
+            if r0 + rows < n:
+                hpdct.decode_i8_f32(frame8[r0 + rows:], frame[r0 + rows:], stream=stream)
+
     def timed(fn, tries=3):
         best = None
         for _ in range(tries):
@@ -811,43 +898,58 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
     forward(y)
     out["gather_ms"] = timed(lambda: gather(y, frame))
     out["gather_bytes_to_root"] = peer_rows * n * 4 if rank == 0 else None
-    forward(y8)
-    out["gather_int8_ms"] = timed(lambda: gather(y8, frame8))
+    forward_i8()
+    out["gather_decode_int8_ms"] = timed(gather_i8)
     out["gather_int8_bytes_to_root"] = peer_rows * n if rank == 0 else None
-    full_dec = torch.empty((n, n), dtype=torch.float32, device=dev) if rank == 0 else None
+    out["decoded_rows_on_root"] = peer_rows if rank == 0 else None
     if rank == 0:
-        dec_ms = _steady_ms(torch, [lambda: hpdct.decode_i8_f32(frame8, full_dec, stream=stream)], reps // 4,
-                            stream)
+        # the decode kernel over a whole frame, from HBM: inputs rotated over
+        # sets_for() int8 frames (>= 4x the Infinity Cache), like every timed kernel
+        nd = sets_for(n * n)
+        q8s = [torch.empty((n, n), dtype=torch.int8, device=dev) for _ in range(nd)]
+        for i, q in enumerate(q8s):
+            xi = torch.empty((n, n), dtype=torch.uint8, device=dev)
+            hpdct.fill_hash_u8(xi, seed=77 + i, first_index=0)
+            hpdct.forward(xi, q)
+            del xi
+        decs = [torch.empty((n, n), dtype=torch.float32, device=dev) for _ in range(nd)]
+        calls = [(lambda i=i: hpdct.decode_i8_f32(q8s[i], decs[i], stream=stream)) for i in range(nd)]
+        dec_ms = _steady_ms(torch, calls, reps // 4, stream)
         out["decode_int8_ms"] = round(dec_ms, 4)
+        out["decode_int8_sets"] = nd
         out["decode_int8_hbm_frac"] = round(5 * n * n / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        del q8s, decs, calls
+        torch.cuda.empty_cache()
 
     def e2e_f32():
         forward(y)
         gather(y, frame)
 
     def e2e_i8():
-        forward(y8)
-        gather(y8, frame8)
-        if rank == 0:
-            hpdct.decode_i8_f32(frame8, full_dec, stream=stream)
+        forward_i8()
+        gather_i8()
 
-    out["end_to_end_ms"] = timed(e2e_f32)
     out["end_to_end_int8_ms"] = timed(e2e_i8)
-    out["end_to_end_note"] = ("slab forward + gather (+ int8 decode on the root) between barriers, host clock, best "
-                              "of 3, max over ranks; compare one_gpu_full_frame_ms (the whole frame on one GPU)")
     if rank == 0:
-        # sharded + gathered == the whole frame computed on one GPU
+        # the frame assembled through the int8 wire equals the one-GPU fp32 forward
         xf = torch.empty((n, n), dtype=torch.uint8, device=dev)
         hpdct.fill_hash_u8(xf, seed=42, first_index=0)
         ref = hpdct.forward(xf)
         torch.cuda.synchronize()
+        out["int8_wire_equals_fp32"] = bool(torch.equal(frame, ref))  # by value: a -0.0 decodes as +0.0
+        del xf
+    out["end_to_end_ms"] = timed(e2e_f32)
+    out["end_to_end_note"] = ("slab forward + gather (int8: the peers' slabs decoded on the root, whose own slab "
+                              "is fp32 in place) between barriers, host clock, best of 3, max over ranks; compare "
+                              "one_gpu_full_frame_ms (the whole frame on one GPU)")
+    if rank == 0:
+        # sharded + gathered == the whole frame computed on one GPU, bit for bit
         out["sharded_equals_unsharded"] = bool(torch.equal(ref.view(torch.int32), frame.view(torch.int32)))
-        out["int8_wire_equals_fp32"] = bool(torch.equal(full_dec, ref))  # by value: a -0.0 decodes as +0.0
-        del xf, ref
+        del ref
     barrier()
     if comm is not None:
         comm.destroy()
-    del x, y, y8, frame, frame8, full_dec
+    del x, y, y8, frame, frame8, own_f32
     torch.cuda.empty_cache()
     return out
 
@@ -898,6 +1000,17 @@ def _c5(args, hpdct, torch, world, rank, barrier, max_over_ranks):
                      "gpx_s_total": round(frames_total * n * n / (ms * 1e-3) / 1e9, 2),
                      "pcie_GBs_per_rank": round(moved / (ms * 1e-3) / 1e9, 1), "pipeline": "streams_2",
                      "by_pipeline_frames_per_s": {k: round(frames_total / (v * 1e-3), 1) for k, v in variants.items()}}
+        # correctness bit: two of the streamed output frames
+        # against hpdct.forward of their pool frame on the device (outside the
+        # timed runs; the copy-only ceiling below overwrites the outputs)
+        ok = True
+        for kf in sorted({0, min(5, mine - 1)}):
+            ref = hpdct.forward(pool_in[kf].to("cuda"), out_dtype=out_dtype)
+            got = pool_out[kf].to("cuda")
+            torch.cuda.synchronize()
+            ok = ok and (torch.equal(got.view(torch.int32), ref.view(torch.int32)) if out_dtype == torch.float32
+                         else torch.equal(got, ref))
+        res[name]["equals_forward"] = bool(ok) if mine > 0 else None
         # the copy-only ceiling: the same H2D and D2H bytes on two streams, no kernel
         dev_in = [torch.empty((n, n), dtype=torch.uint8, device="cuda") for _ in range(2)]
         dev_out = [torch.empty((n, n), dtype=out_dtype, device="cuda") for _ in range(2)]

@@ -4,17 +4,25 @@
 // ncclSend / ncclRecv pairs inside one group (rccl.h:700,722), which also
 // covers slabs that differ by a tile row (ncclGather, rccl.h:745, needs equal
 // counts).  Bytes travel as ncclUint8: the element type does not matter to a
-// gather.  Before the first gather of a geometry, the ranks check that they
-// agree on it (hpdct_dist_geometry.hpp): a disagreement is an error on every
-// rank instead of sends and receives of different sizes that never complete.
+// gather.  The ranks check that they agree on a gather before anything is
+// posted (hpdct_dist_geometry.hpp), so a disagreement is an error instead of
+// sends and receives of different sizes that never complete:
+//   - communicators of one hpdct_comm_init_all (one thread, one group): their
+//     gathers are queued, compared on the host at hpdct_group_end and posted
+//     there only if every communicator asked for the same gathers;
+//   - a per-process communicator: one 64-byte max all-reduce before the first
+//     gather of a geometry it has not agreed on yet (see hpdct_dist.h for what
+//     that covers).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "hpdct.h"
 #include "hpdct_dist.h"
@@ -24,15 +32,47 @@
 static_assert(HPDCT_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "hpdct_unique_id size");
 
 namespace {
-// Communicators of one hpdct_comm_init_all call live in this process: each
-// round of gathers (one per communicator, normally inside one
-// hpdct_group_start/end) is compared on the host, no collective needed.
+using hpdct::dist::Post;
+using hpdct::dist::RootSlab;
+
+// The root's int8 -> fp32 decode of the peer rows of a gather-decode: launched
+// after the receives are enqueued, i.e. after the outermost ncclGroupEnd.
+struct DecodeJob {
+    int device;
+    hipStream_t s;
+    const int8_t* src;
+    float* dst;
+    int64_t n;
+};
+
+// One gather call, ready to post.
+struct Pending {
+    struct hpdct_comm_s* comm;
+    std::vector<Post> plan;
+    const char* slab;
+    char* frame;
+    hipStream_t s;
+    std::vector<DecodeJob> decodes;
+};
+
+// Communicators of one hpdct_comm_init_all call live in this process: the
+// gathers of a group are queued per communicator and compared on the host
+// at hpdct_group_end (hpdct::dist::clique_round_agrees), no collective needed.
 struct Clique {
     std::mutex m;
-    int reported = 0;  // gathers of the current round so far
-    hpdct::dist::Geometry g{};
+    std::vector<std::vector<hpdct::dist::Geometry>> asked;  // per communicator rank, in call order
+    std::vector<bool> failed;                               // a call of that communicator failed validation
+    std::vector<Pending> queued;
+    explicit Clique(int n) : asked(n), failed(n, false) {}
+    void clear() {
+        for (auto& a : asked) a.clear();
+        std::fill(failed.begin(), failed.end(), false);
+        queued.clear();
+    }
 };
 thread_local int t_group_depth = 0;
+thread_local std::vector<std::shared_ptr<Clique>> t_cliques;  // cliques with gathers in the open group
+thread_local std::vector<DecodeJob> t_decodes;                // decodes waiting for the outermost group end
 }  // namespace
 
 struct hpdct_comm_s {
@@ -73,13 +113,6 @@ struct DeviceScope {
     }
 };
 
-// (first_row, rows) of every rank, as hpdct_shard_rows
-void shard(int64_t height, int world, int rank, int64_t& first, int64_t& rows) {
-    const int64_t tile_rows = height / 8, base = tile_rows / world, extra = tile_rows % world;
-    first = (rank * base + (rank < extra ? rank : extra)) * 8;
-    rows = (base + (rank < extra ? 1 : 0)) * 8;
-}
-
 hpdct_status check_geometry(hpdct_comm comm, int64_t height, int64_t width) {
     if (!comm) return fail(HPDCT_ERROR_INVALID_VALUE, "null communicator");
     if (height <= 0 || width <= 0 || height % 8 || width % 8)
@@ -90,20 +123,10 @@ hpdct_status check_geometry(hpdct_comm comm, int64_t height, int64_t width) {
     return HPDCT_SUCCESS;
 }
 
-// The ranks agree on this gather's geometry (see the file comment).
-// (A one-rank per-process communicator runs the check too: it is once per
-// geometry, and it keeps the all-reduce path exercised on a one-GPU box.)
+// A per-process communicator: the ranks agree on this gather's geometry (see
+// the file comment).  A one-rank communicator runs the check too: it is once
+// per geometry, and it keeps the all-reduce path exercised on a one-GPU box.
 hpdct_status check_agreement(hpdct_comm comm, const hpdct::dist::Geometry& g, hipStream_t s) {
-    if (comm->clique) {
-        Clique& c = *comm->clique;
-        std::lock_guard<std::mutex> lock(c.m);
-        if (c.reported == 0) c.g = g;  // the round's first gather sets the geometry
-        const bool same = c.g == g;
-        if (++c.reported == comm->size) c.reported = 0;  // round complete
-        if (same) return HPDCT_SUCCESS;
-        return fail(HPDCT_ERROR_INVALID_VALUE,
-                    "gathers of one round disagree on (height, width, type, root) across the communicators");
-    }
     if (comm->agreed.contains(g)) return HPDCT_SUCCESS;
     if (t_group_depth > 0)
         return fail(HPDCT_ERROR_INVALID_VALUE,
@@ -138,6 +161,119 @@ hpdct_status check_agreement(hpdct_comm comm, const hpdct::dist::Geometry& g, hi
     return HPDCT_SUCCESS;
 }
 
+// Posts one gather's operations (inside the caller's ncclGroupStart/End).
+hpdct_status post_plan(const Pending& p) {
+    DeviceScope ds(p.comm->device);
+    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    for (const Post& o : p.plan) {
+        hpdct_status st = HPDCT_SUCCESS;
+        switch (o.kind) {
+            case Post::kSend:
+                st = nccl_status(ncclSend(p.slab, o.bytes, ncclUint8, o.peer, p.comm->nccl, p.s), "ncclSend");
+                break;
+            case Post::kRecv:
+                st = nccl_status(ncclRecv(p.frame + o.offset, o.bytes, ncclUint8, o.peer, p.comm->nccl, p.s),
+                                 "ncclRecv");
+                break;
+            case Post::kCopy:
+                if (p.frame + o.offset != p.slab)
+                    st = hip_status(hipMemcpyAsync(p.frame + o.offset, p.slab, o.bytes, hipMemcpyDeviceToDevice, p.s),
+                                    "hipMemcpyAsync");
+                break;
+        }
+        if (st != HPDCT_SUCCESS) return st;
+    }
+    return HPDCT_SUCCESS;
+}
+
+hpdct_status run_decodes(std::vector<DecodeJob>& jobs) {
+    hpdct_status first = HPDCT_SUCCESS;
+    for (const DecodeJob& j : jobs) {
+        DeviceScope ds(j.device);
+        hpdct_status st = ds.err != hipSuccess ? hip_status(ds.err, "hipSetDevice")
+                                               : hpdct_decode_i8_f32(j.src, j.dst, j.n, j.s);
+        if (first == HPDCT_SUCCESS) first = st;
+    }
+    jobs.clear();
+    return first;
+}
+
+// The shared part of the gathers: validation, agreement, then the posts now
+// (per-process communicator, or a lone init_all communicator outside a group)
+// or queued for hpdct_group_end (init_all communicators inside a group).
+hpdct_status gather(hpdct_comm comm, const void* d_slab, void* d_frame, hpdct_dtype type, int64_t height,
+                    int64_t width, int root, void* stream, RootSlab own, float* d_frame_f32) {
+    hpdct_status st = check_geometry(comm, height, width);
+    const bool defer = st == HPDCT_SUCCESS && comm->clique && t_group_depth > 0;
+    auto note_failure = [&](hpdct_status e) {
+        if (comm && comm->clique && t_group_depth > 0) {
+            // the round fails as a whole: nothing of it is posted at group end
+            std::lock_guard<std::mutex> lock(comm->clique->m);
+            comm->clique->failed[comm->rank] = true;
+            if (std::find(t_cliques.begin(), t_cliques.end(), comm->clique) == t_cliques.end())
+                t_cliques.push_back(comm->clique);
+        }
+        return e;
+    };
+    if (st != HPDCT_SUCCESS) return note_failure(st);
+    if (type != HPDCT_F32 && type != HPDCT_I8 && type != HPDCT_U8)
+        return note_failure(fail(HPDCT_ERROR_UNSUPPORTED, "gather type must be HPDCT_F32, HPDCT_I8 or HPDCT_U8"));
+    if (root < 0 || root >= comm->size) return note_failure(fail(HPDCT_ERROR_INVALID_VALUE, "root out of range"));
+    if (comm->rank != root && !d_slab) return note_failure(fail(HPDCT_ERROR_INVALID_VALUE, "null slab pointer"));
+    if (comm->rank == root && own != RootSlab::kSkip && !d_slab)
+        return note_failure(fail(HPDCT_ERROR_INVALID_VALUE, "null slab pointer"));
+    if (comm->rank == root && !d_frame) return note_failure(fail(HPDCT_ERROR_INVALID_VALUE, "null frame pointer on the root"));
+    if (comm->rank == root && own == RootSlab::kSkip && !d_frame_f32)
+        return note_failure(fail(HPDCT_ERROR_INVALID_VALUE, "null fp32 frame pointer on the root"));
+    if (comm->clique && comm->size > 1 && t_group_depth == 0)
+        return fail(HPDCT_ERROR_INVALID_VALUE,
+                    "gathers on communicators of hpdct_comm_init_all go between hpdct_group_start and "
+                    "hpdct_group_end (one thread drives every device)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const hpdct::dist::Geometry geo{{height, width, static_cast<int64_t>(type), root}};
+
+    Pending p{comm, {}, static_cast<const char*>(d_slab), static_cast<char*>(d_frame), s, {}};
+    // one rank whose slab already sits in the frame, or is not gathered: nothing moves
+    const RootSlab eff = own == RootSlab::kCopy && d_frame == d_slab ? RootSlab::kInPlace : own;
+    p.plan = hpdct::dist::gather_plan(height, width, elem_size(type), comm->size, root, comm->rank, eff);
+    if (comm->rank == root && own == RootSlab::kSkip) {
+        // decode the peer rows: the slabs before the root's and after it are contiguous
+        int64_t first, rows;
+        hpdct::dist::shard_rows(height, comm->size, root, first, rows);
+        const int8_t* q = static_cast<const int8_t*>(d_frame);
+        if (first > 0) p.decodes.push_back({comm->device, s, q, d_frame_f32, first * width});
+        if (first + rows < height)
+            p.decodes.push_back({comm->device, s, q + (first + rows) * width, d_frame_f32 + (first + rows) * width,
+                                 (height - first - rows) * width});
+    }
+
+    if (defer) {
+        Clique& c = *comm->clique;
+        std::lock_guard<std::mutex> lock(c.m);
+        c.asked[comm->rank].push_back(geo);
+        c.queued.push_back(std::move(p));
+        if (std::find(t_cliques.begin(), t_cliques.end(), comm->clique) == t_cliques.end())
+            t_cliques.push_back(comm->clique);
+        return HPDCT_SUCCESS;
+    }
+    DeviceScope ds(comm->device);
+    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
+    if (!comm->clique) {
+        if (hpdct_status e = check_agreement(comm, geo, s)) return e;
+    }
+    if (p.plan.empty() && p.decodes.empty()) return HPDCT_SUCCESS;
+    if (hpdct_status e = nccl_status(ncclGroupStart(), "ncclGroupStart")) return e;
+    st = post_plan(p);
+    const hpdct_status end = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    if (st == HPDCT_SUCCESS) st = end;
+    if (st != HPDCT_SUCCESS) return st;
+    if (t_group_depth > 0) {  // the receives are enqueued at the outermost group end
+        t_decodes.insert(t_decodes.end(), p.decodes.begin(), p.decodes.end());
+        return HPDCT_SUCCESS;
+    }
+    return run_decodes(p.decodes);
+}
+
 }  // namespace
 
 extern "C" {
@@ -146,7 +282,7 @@ hpdct_status hpdct_shard_rows(int64_t height, int world, int rank, int64_t* firs
     if (!first_row || !rows) return fail(HPDCT_ERROR_INVALID_VALUE, "null output pointer");
     if (height <= 0 || height % 8) return fail(HPDCT_ERROR_INVALID_VALUE, "height must be a positive multiple of 8");
     if (world < 1 || rank < 0 || rank >= world) return fail(HPDCT_ERROR_INVALID_VALUE, "rank out of range");
-    shard(height, world, rank, *first_row, *rows);
+    hpdct::dist::shard_rows(height, world, rank, *first_row, *rows);
     return HPDCT_SUCCESS;
 }
 
@@ -161,7 +297,7 @@ hpdct_status hpdct_comm_init_all(hpdct_comm* comms, int ndev, const int* devices
         return st;
     }
     bool ok = true;
-    std::shared_ptr<Clique> clique(new (std::nothrow) Clique());
+    std::shared_ptr<Clique> clique(new (std::nothrow) Clique(ndev));
     ok = clique != nullptr;
     for (int i = 0; i < ndev && ok; ++i) {
         comms[i] = new (std::nothrow) hpdct_comm_s{raw[i], i, ndev, devices[i], clique, {}, nullptr};
@@ -220,20 +356,58 @@ int hpdct_comm_size(hpdct_comm comm) { return comm ? comm->size : -1; }
 int hpdct_comm_device(hpdct_comm comm) { return comm ? comm->device : -1; }
 
 hpdct_status hpdct_group_start(void) {
+    if (t_group_depth == 0) {  // a new group: no round of an earlier (abandoned) group survives
+        for (auto& c : t_cliques) {
+            std::lock_guard<std::mutex> lock(c->m);
+            c->clear();
+        }
+        t_cliques.clear();
+        t_decodes.clear();
+    }
     const hpdct_status st = nccl_status(ncclGroupStart(), "ncclGroupStart");
     if (st == HPDCT_SUCCESS) ++t_group_depth;
     return st;
 }
+
 hpdct_status hpdct_group_end(void) {
     if (t_group_depth > 0) --t_group_depth;
-    return nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    hpdct_status st = HPDCT_SUCCESS;
+    if (t_group_depth == 0) {
+        // each clique's round: posted whole if its communicators agree, else not at all
+        for (auto& cp : t_cliques) {
+            Clique& c = *cp;
+            std::lock_guard<std::mutex> lock(c.m);
+            if (!hpdct::dist::clique_round_agrees(c.asked, c.failed)) {
+                if (st == HPDCT_SUCCESS)
+                    st = fail(HPDCT_ERROR_INVALID_VALUE,
+                              "the gathers of this group disagree across the communicators (or one failed its "
+                              "checks): nothing was posted");
+            } else {
+                for (const Pending& p : c.queued) {
+                    const hpdct_status e = post_plan(p);
+                    if (st == HPDCT_SUCCESS) st = e;
+                    t_decodes.insert(t_decodes.end(), p.decodes.begin(), p.decodes.end());
+                }
+            }
+            c.clear();
+        }
+        t_cliques.clear();
+    }
+    const hpdct_status end = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    if (st == HPDCT_SUCCESS) st = end;
+    if (t_group_depth == 0) {
+        // the receives are enqueued now: the decodes go behind them on their streams
+        const hpdct_status d = st == HPDCT_SUCCESS ? run_decodes(t_decodes) : (t_decodes.clear(), HPDCT_SUCCESS);
+        if (st == HPDCT_SUCCESS) st = d;
+    }
+    return st;
 }
 
 hpdct_status hpdct_forward_slab(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,
                                 int64_t height, int64_t width, void* stream) {
     if (hpdct_status st = check_geometry(comm, height, width)) return st;
     int64_t first, rows;
-    shard(height, comm->size, comm->rank, first, rows);
+    hpdct::dist::shard_rows(height, comm->size, comm->rank, first, rows);
     DeviceScope ds(comm->device);
     if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
     return hpdct_forward(d_slab, HPDCT_U8, d_coef_slab, out_type, rows, width, nullptr, 0u, stream);
@@ -241,42 +415,12 @@ hpdct_status hpdct_forward_slab(hpdct_comm comm, const uint8_t* d_slab, void* d_
 
 hpdct_status hpdct_gather_rows(hpdct_comm comm, const void* d_slab, void* d_frame, hpdct_dtype type, int64_t height,
                                int64_t width, int root, void* stream) {
-    if (hpdct_status st = check_geometry(comm, height, width)) return st;
-    if (type != HPDCT_F32 && type != HPDCT_I8 && type != HPDCT_U8)
-        return fail(HPDCT_ERROR_UNSUPPORTED, "gather type must be HPDCT_F32, HPDCT_I8 or HPDCT_U8");
-    if (root < 0 || root >= comm->size) return fail(HPDCT_ERROR_INVALID_VALUE, "root out of range");
-    if (!d_slab) return fail(HPDCT_ERROR_INVALID_VALUE, "null slab pointer");
-    if (comm->rank == root && !d_frame) return fail(HPDCT_ERROR_INVALID_VALUE, "null frame pointer on the root");
-    const size_t row_bytes = static_cast<size_t>(width) * elem_size(type);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    DeviceScope ds(comm->device);
-    if (ds.err != hipSuccess) return hip_status(ds.err, "hipSetDevice");
-    const hpdct::dist::Geometry geo{{height, width, static_cast<int64_t>(type), root}};
-    if (hpdct_status st = check_agreement(comm, geo, s)) return st;
-    // one rank whose slab already sits in the frame: nothing moves
-    if (comm->size == 1 && d_frame == d_slab) return HPDCT_SUCCESS;
-    int64_t first, rows;
-    if (comm->rank != root) {
-        shard(height, comm->size, comm->rank, first, rows);
-        return nccl_status(ncclSend(d_slab, static_cast<size_t>(rows) * row_bytes, ncclUint8, root, comm->nccl, s),
-                           "ncclSend");
-    }
-    char* frame = static_cast<char*>(d_frame);
-    if (hpdct_status st = nccl_status(ncclGroupStart(), "ncclGroupStart")) return st;
-    hpdct_status st = HPDCT_SUCCESS;
-    for (int r = 0; r < comm->size && st == HPDCT_SUCCESS; ++r) {
-        shard(height, comm->size, r, first, rows);
-        char* dst = frame + static_cast<size_t>(first) * row_bytes;
-        const size_t bytes = static_cast<size_t>(rows) * row_bytes;
-        if (r == root) {
-            if (dst != d_slab)
-                st = hip_status(hipMemcpyAsync(dst, d_slab, bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
-        } else {
-            st = nccl_status(ncclRecv(dst, bytes, ncclUint8, r, comm->nccl, s), "ncclRecv");
-        }
-    }
-    const hpdct_status end = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
-    return st != HPDCT_SUCCESS ? st : end;
+    return gather(comm, d_slab, d_frame, type, height, width, root, stream, RootSlab::kCopy, nullptr);
+}
+
+hpdct_status hpdct_gather_decode_i8(hpdct_comm comm, const int8_t* d_slab, int8_t* d_frame_i8, float* d_frame_f32,
+                                    int64_t height, int64_t width, int root, void* stream) {
+    return gather(comm, d_slab, d_frame_i8, HPDCT_I8, height, width, root, stream, RootSlab::kSkip, d_frame_f32);
 }
 
 hpdct_status hpdct_forward_sharded(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,

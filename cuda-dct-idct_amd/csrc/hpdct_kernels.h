@@ -83,6 +83,10 @@ hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t fi
 // int8 wire coefficients -> fp32 plane (hpdct_decode.hip)
 hipError_t launch_decode_i8_f32(const int8_t* in, float* out, uint64_t n, hipStream_t s);
 
+// hpdct_floor_probe (hpdct_probe.hip): kind 0 an empty kernel, 1 a u8 -> fp32
+// copy, both on the grid the uint8 -> fp32 forward of g launches
+hipError_t launch_floor_probe(int kind, const uint8_t* in, float* out, const TileGrid& g, hipStream_t s);
+
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.
 int mapping_mode();
 

@@ -37,6 +37,15 @@ RtSums* slot_for(int dev, const void* sums, hipStream_t s) {
     if (d.used == kSlotChunk) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        // relaxed capture mode for this thread while it allocates and
+        // synchronises: a stream capture another thread runs in global mode
+        // is then left intact
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        if (hipThreadExchangeStreamCaptureMode(&mode) != hipSuccess) return nullptr;
+        struct Restore {
+            hipStreamCaptureMode m;
+            ~Restore() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+        } restore{mode};
         if (!d.zero_stream && hipStreamCreateWithFlags(&d.zero_stream, hipStreamNonBlocking) != hipSuccess) {
             d.zero_stream = nullptr;
             return nullptr;
@@ -57,9 +66,12 @@ RtSums* slot_for(int dev, const void* sums, hipStream_t s) {
     return slot;
 }
 
-// a launch that failed after the round trip was queued may leave its slot
-// non-zero: the pointer gets a fresh slot next time
-void drop_slot(int dev, const void* sums) {
+// A launch that failed after the round trip was queued may leave its slot
+// non-zero.  The slot is zeroed behind it on the same stream, so the pointer
+// keeps its slot (a graph captured earlier with that slot stays correct);
+// only when even that fails does the pointer get a fresh slot next time.
+void recover_slot(int dev, const void* sums, RtSums* slot, hipStream_t s) {
+    if (hipMemsetAsync(slot, 0, sizeof(RtSums), s) == hipSuccess) return;
     std::lock_guard<std::mutex> lock(g_slot_mutex);
     g_slots[dev].by_sums.erase(sums);
 }
@@ -72,7 +84,7 @@ hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int re
     RtSums* slot = nullptr;
     if (sums && zero_sums && hipGetDevice(&dev) == hipSuccess) slot = slot_for(dev, sums, s);
     const hipError_t e = launch_roundtrip_impl(img, coef, recon, recon_kind, sums, g, qp, fast, s, zero_sums, slot);
-    if (e != hipSuccess && slot) drop_slot(dev, sums);
+    if (e != hipSuccess && slot) recover_slot(dev, sums, slot, s);
     return e;
 }
 

@@ -279,8 +279,11 @@ hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, cons
 // Sums: zero_sums false adds into *sums; else with a slot (all zero, kept for
 // this sums pointer by the caller of this function) the kernel adds into the
 // slot and rt_finish_kernel moves it over *sums, and without one a memset
-// zeroes *sums before the kernel.
-inline hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
+// zeroes *sums before the kernel.  A template, so that a translation unit
+// including this header for the kernels alone does not instantiate (and
+// compile) every round-trip variant.
+template <int = 0>
+hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
                                         RtSums* sums, const TileGrid& g, const QParams& qp, int fast,
                                         hipStream_t s, bool zero_sums = true, RtSums* slot = nullptr) {
     RtSums* const acc = sums && zero_sums && slot ? slot : sums;

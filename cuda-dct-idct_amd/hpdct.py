@@ -51,6 +51,7 @@ C_SYMBOLS = [
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
     "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate", "hpdct_forward_frames",
     "hpdct_stream_create", "hpdct_stream_run", "hpdct_stream_destroy", "hpdct_decode_i8_f32",
+    "hpdct_floor_probe",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -103,6 +104,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_build_info.restype = ctypes.c_char_p
     lib.hpdct_decode_i8_f32.argtypes = [vp, vp, i64, vp]
     lib.hpdct_decode_i8_f32.restype = ctypes.c_int
+    lib.hpdct_floor_probe.argtypes = [ctypes.c_int, vp, vp, i64, i64, vp]
+    lib.hpdct_floor_probe.restype = ctypes.c_int
     lib.hpdct_status_string.restype = ctypes.c_char_p
     lib.hpdct_status_string.argtypes = [ctypes.c_int]
     lib.hpdct_last_error_string.restype = ctypes.c_char_p
@@ -615,6 +618,34 @@ def decode_i8_f32(q, out=None, stream=None):
     return out
 
 
+PROBE_EMPTY, PROBE_COPY = 0, 1
+
+
+def bind_floor_probe(kind: int, img=None, out=None, height: int = 0, width: int = 0, stream=None):
+    """Measurement floor of the uint8 -> fp32 forward of a height x width
+    frame (hpdct_floor_probe), as a zero-argument callable like bind():
+    PROBE_EMPTY an empty kernel on that forward's grid, PROBE_COPY the same
+    grid copying img (uint8) to out as fp32."""
+    torch = _torch()
+    ip = op = None
+    if kind == PROBE_COPY:
+        _device_plane(img, "img", None, int(height) * int(width), (torch.uint8,))
+        _device_plane(out, "out", img.device, int(height) * int(width), (torch.float32,))
+        ip, op = ctypes.c_void_p(img.data_ptr()), ctypes.c_void_p(out.data_ptr())
+    fn = load_library().hpdct_floor_probe
+    args = (int(kind), ip, op, int(height), int(width), _stream_ptr(stream))
+
+    def call():
+        st = fn(*args)
+        if st:
+            _check(st)
+    return call
+
+
+def floor_probe(kind: int, img=None, out=None, height: int = 0, width: int = 0, stream=None) -> None:
+    bind_floor_probe(kind, img, out, height, width, stream)()
+
+
 # ---------------------------------------------------------------------------
 # the reference's own C++ entry points (compat layer, synchronous, prints)
 # ---------------------------------------------------------------------------
@@ -690,6 +721,7 @@ DIST_SYMBOLS = [
     "hpdct_shard_rows", "hpdct_comm_init_all", "hpdct_comm_unique_id", "hpdct_comm_init_rank",
     "hpdct_comm_destroy", "hpdct_comm_rank", "hpdct_comm_size", "hpdct_comm_device",
     "hpdct_group_start", "hpdct_group_end", "hpdct_forward_slab", "hpdct_gather_rows", "hpdct_forward_sharded",
+    "hpdct_gather_decode_i8",
 ]
 UNIQUE_ID_BYTES = 128
 _dist = None
@@ -722,6 +754,7 @@ def load_dist_library() -> ctypes.CDLL:
     lib.hpdct_forward_slab.argtypes = [vp, vp, vp, ci, i64, i64, vp]
     lib.hpdct_gather_rows.argtypes = [vp, vp, vp, ci, i64, i64, ci, vp]
     lib.hpdct_forward_sharded.argtypes = [vp, vp, vp, ci, vp, i64, i64, ci, vp]
+    lib.hpdct_gather_decode_i8.argtypes = [vp, vp, vp, vp, i64, i64, ci, vp]
     for name in DIST_SYMBOLS:
         if name not in ("hpdct_comm_rank", "hpdct_comm_size", "hpdct_comm_device"):
             getattr(lib, name).restype = ci
@@ -819,3 +852,25 @@ def gather_rows(comm: Comm, slab, frame, height: int, width: int, root: int = 0,
     _check(load_dist_library().hpdct_gather_rows(comm.handle, ctypes.c_void_p(slab.data_ptr()), fp,
                                                  _dtype_code(slab), int(height), int(width), int(root),
                                                  _stream_ptr(stream)))
+
+
+def gather_decode_i8(comm: Comm, slab8, frame8, frame, height: int, width: int, root: int = 0,
+                     stream=None) -> None:
+    """The int8 wire format's gather (hpdct_gather_decode_i8): every rank but
+    the root sends its int8 slab; the root, whose own slab is already fp32 at
+    its rows of `frame` (pass slab8=None there), receives the peers' slabs
+    into the int8 scratch `frame8` and decodes them into `frame`.  frame8 and
+    frame are ignored (may be None) off the root."""
+    torch = _torch()
+    n = int(height) * int(width)
+    sp = f8 = ff = None
+    if comm.rank != root:
+        _, rows = shard_rows_native(height, comm.size, comm.rank)
+        _device_plane(slab8, "slab", None, rows * int(width), (torch.int8,))
+        sp = ctypes.c_void_p(slab8.data_ptr())
+    else:
+        _device_plane(frame8, "frame8", None, n, (torch.int8,))
+        _device_plane(frame, "frame", frame8.device, n, (torch.float32,))
+        f8, ff = ctypes.c_void_p(frame8.data_ptr()), ctypes.c_void_p(frame.data_ptr())
+    _check(load_dist_library().hpdct_gather_decode_i8(comm.handle, sp, f8, ff, int(height), int(width), int(root),
+                                                      _stream_ptr(stream)))

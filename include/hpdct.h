@@ -235,6 +235,17 @@ hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_
  * `stream`.  No reference counterpart (the reference has no int8 format). */
 hpdct_status hpdct_decode_i8_f32(const int8_t* d_q, float* d_out, int64_t n, void* stream);
 
+/* Measurement floors of the uint8 -> fp32 forward of a height x width frame
+ * (no reference counterpart; bench.py's C2 leg): kind HPDCT_PROBE_EMPTY
+ * launches an empty kernel on the grid and workgroup size that forward uses
+ * (d_in, d_out unused, may be NULL), HPDCT_PROBE_COPY the same grid copying
+ * the frame's bytes: d_out[i] = (float)d_in[i], 1 B read + 4 B non-temporal
+ * write per pixel and no transform.  Device pointers d_in 8-byte, d_out
+ * 16-byte aligned.  Async on `stream`. */
+typedef enum hpdct_probe_kind { HPDCT_PROBE_EMPTY = 0, HPDCT_PROBE_COPY = 1 } hpdct_probe_kind;
+hpdct_status hpdct_floor_probe(hpdct_probe_kind kind, const uint8_t* d_in, float* d_out, int64_t height,
+                               int64_t width, void* stream);
+
 /* Work mapping of the kernels (new; the reference has one fixed decomposition
  * per program).  Output is bit-identical in every mapping; only speed differs.
  *   AUTO   per frame: eight lanes per 8x8 tile ("octet") for frames below

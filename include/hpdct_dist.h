@@ -28,6 +28,20 @@
  * hpdct_forward_sharded) of all its communicators between
  * hpdct_group_start() and hpdct_group_end() (ncclGroupStart/End), exactly
  * as RCCL requires for single-thread multi-device use.
+ *
+ * Agreement (a gather whose ranks disagree on its size would post sends and
+ * receives that never complete):
+ *   - communicators of one hpdct_comm_init_all: the gathers of a group are
+ *     queued and compared at hpdct_group_end; they are posted only when every
+ *     communicator asked for the same gathers in the same order and none of
+ *     the calls failed its checks, otherwise nothing is posted and
+ *     hpdct_group_end returns the error;
+ *   - per-process communicators (hpdct_comm_init_rank): one 64-byte max
+ *     all-reduce before the first gather of a (height, width, type, root) the
+ *     communicator has not agreed on yet.  It catches ranks that disagree on
+ *     that first gather of a new geometry; ranks that later mix an agreed
+ *     geometry with a new one on the same call are not caught (the caller
+ *     keeps the ranks' call sequences alike, as for any collective).
  */
 #ifndef HPDCT_DIST_H
 #define HPDCT_DIST_H
@@ -84,6 +98,20 @@ hpdct_status hpdct_forward_slab(hpdct_comm comm, const uint8_t* d_slab, void* d_
  * place in d_frame.  Asynchronous on `stream`. */
 hpdct_status hpdct_gather_rows(hpdct_comm comm, const void* d_slab, void* d_frame, hpdct_dtype type, int64_t height,
                                int64_t width, int root, void* stream);
+
+/* The int8 wire format's gather: every rank but the
+ * root passes its int8 coefficient slab (d_slab, from hpdct_forward_slab with
+ * HPDCT_I8); the root has already written its own slab as fp32 at its rows of
+ * d_frame_f32 (hpdct_forward of its slab into d_frame_f32 + first_row * width)
+ * and passes d_slab = NULL.  The root receives the peers' slabs into
+ * d_frame_i8 (a height x width int8 scratch frame; the root's rows are not
+ * touched) and decodes them into d_frame_f32 (hpdct_decode_i8_f32: at most two
+ * launches, the rows before and after its own slab), so d_frame_f32 ends as
+ * the fp32 frame of a one-GPU hpdct_forward, bit for bit.  Asynchronous on
+ * `stream`; inside hpdct_group_start/end the decodes are issued at the
+ * outermost hpdct_group_end, behind the receives. */
+hpdct_status hpdct_gather_decode_i8(hpdct_comm comm, const int8_t* d_slab, int8_t* d_frame_i8, float* d_frame_f32,
+                                    int64_t height, int64_t width, int root, void* stream);
 
 /* hpdct_forward_slab then hpdct_gather_rows of the coefficient slab. */
 hpdct_status hpdct_forward_sharded(hpdct_comm comm, const uint8_t* d_slab, void* d_coef_slab, hpdct_dtype out_type,

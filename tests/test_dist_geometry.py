@@ -90,3 +90,134 @@ def test_library_uses_the_check():
     assert '#include "hpdct_dist_geometry.hpp"' in src
     assert "check_agreement(comm, geo, s)" in src
     assert "ncclAllReduce(comm->d_check, comm->d_check, hpdct::dist::kCheckWords" in src
+
+
+# ---- the posts of one gather (hpdct::dist::gather_plan, hpdct_dist.cpp's
+# gather) and the init_all group check (clique_round_agrees) -----------------
+PLAN_DRIVER = r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "hpdct_dist_geometry.hpp"
+using namespace hpdct::dist;
+// plan <height> <width> <elem> <world> <root> <rank> <own: 0 copy, 1 in place, 2 skip>
+// round <n_comms> then per comm: <failed> <count> <count x (h w type root)>
+int main(int argc, char** argv) {
+    if (argc > 1 && !strcmp(argv[1], "plan")) {
+        const auto plan = gather_plan(atoll(argv[2]), atoll(argv[3]), (size_t)atoll(argv[4]), atoi(argv[5]),
+                                      atoi(argv[6]), atoi(argv[7]), (RootSlab)atoi(argv[8]));
+        for (const Post& p : plan)
+            printf("%d %d %lld %lld %llu %llu\n", (int)p.kind, p.peer, (long long)p.first_row, (long long)p.rows,
+                   (unsigned long long)p.offset, (unsigned long long)p.bytes);
+        return 0;
+    }
+    if (argc > 1 && !strcmp(argv[1], "round")) {
+        int a = 2;
+        const int n = atoi(argv[a++]);
+        std::vector<std::vector<Geometry>> asked(n);
+        std::vector<bool> failed(n);
+        for (int c = 0; c < n; ++c) {
+            failed[c] = atoi(argv[a++]) != 0;
+            const int cnt = atoi(argv[a++]);
+            for (int i = 0; i < cnt; ++i, a += 4)
+                asked[c].push_back(Geometry{{atoll(argv[a]), atoll(argv[a + 1]), atoll(argv[a + 2]), atoll(argv[a + 3])}});
+        }
+        printf("%s\n", clique_round_agrees(asked, failed) ? "post" : "refuse");
+        return 0;
+    }
+    return 2;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def plan_driver(tmp_path_factory):
+    d = tmp_path_factory.mktemp("plan")
+    src = d / "plan.cpp"
+    src.write_text(PLAN_DRIVER)
+    exe = d / "plan"
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-I", CSRC, str(src), "-o", str(exe)], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    return str(exe)
+
+
+def _plan(exe, height, width, elem, world, root, rank, own):
+    r = subprocess.run([exe, "plan"] + [str(v) for v in (height, width, elem, world, root, rank, own)],
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    return [tuple(int(x) for x in line.split()) for line in r.stdout.split("\n") if line.strip()]
+
+
+def _shard(height, world, rank):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("hpdct_dist_py", os.path.join(ROOT, "cuda-dct-idct_amd",
+                                                                                 "hpdct_dist.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.shard_rows(height, world, rank)
+
+
+SEND, RECV, COPY = 0, 1, 2
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("height", [16384, 16384 + 8 * 3, 8 * 8 + 8 * 5, 8 * 11])
+@pytest.mark.parametrize("elem", [4, 1])
+def test_gather_plan_every_post(plan_driver, world, height, elem):
+    """Every (rank, first, rows, bytes) each rank posts, for equal and ragged
+    slabs, every root, the root's own slab copied, in place or skipped (the
+    int8 gather-decode): sends carry exactly the slab, the root receives every
+    peer's rows at their offset, and the frame is tiled without gap or overlap."""
+    if height // 8 < world:
+        pytest.skip("fewer tile rows than ranks is refused by check_geometry")
+    width = 8 * 7
+    row_bytes = width * elem
+    for root in range(world):
+        for own in (0, 1, 2):
+            covered = []
+            for rank in range(world):
+                plan = _plan(plan_driver, height, width, elem, world, root, rank, own)
+                first, rows = _shard(height, world, rank)
+                if rank != root:
+                    assert plan == [(SEND, root, first, rows, 0, rows * row_bytes)]
+                    continue
+                expect = []
+                for r in range(world):
+                    f, n = _shard(height, world, r)
+                    if r != root:
+                        expect.append((RECV, r, f, n, f * row_bytes, n * row_bytes))
+                    elif own == 0:
+                        expect.append((COPY, r, f, n, f * row_bytes, n * row_bytes))
+                assert plan == expect
+                covered = [(p[4], p[4] + p[5]) for p in plan]
+            if own != 0:  # the root's own rows are the one hole
+                f, n = _shard(height, world, root)
+                covered.append((f * row_bytes, (f + n) * row_bytes))
+            covered.sort()
+            assert covered[0][0] == 0 and covered[-1][1] == height * row_bytes
+            assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+
+
+def _round(exe, comms):
+    args = ["round", str(len(comms))]
+    for failed, geos in comms:
+        args += [str(int(failed)), str(len(geos))]
+        for g in geos:
+            args += [str(v) for v in g]
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def test_clique_round_posts_only_when_all_agree(plan_driver):
+    """an init_all group is posted only when every communicator was
+    asked for the same gathers in the same order and none failed its checks;
+    interleaved rounds (fp32 then int8 on every communicator) are fine."""
+    f32, i8 = (16384, 16384, 2, 0), (16384, 16384, 1, 0)
+    assert _round(plan_driver, [(False, [f32])] * 8) == "post"
+    assert _round(plan_driver, [(False, [f32, i8])] * 4) == "post"
+    assert _round(plan_driver, [(False, [f32, i8])] * 3 + [(False, [i8, f32])]) == "refuse"
+    assert _round(plan_driver, [(False, [f32])] * 3 + [(False, [])]) == "refuse"  # one communicator missing
+    assert _round(plan_driver, [(False, [f32])] * 3 + [(True, [])]) == "refuse"   # one call failed its checks
+    assert _round(plan_driver, [(False, [f32])] * 2 + [(False, [(16384, 16384, 2, 1)])]) == "refuse"

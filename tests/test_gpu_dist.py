@@ -149,6 +149,73 @@ def test_world1_gather_rejects_bad_root(hp, dev, comm1):
         hp.gather_rows(comm1, s, s.clone(), 64, 64, root=1)
 
 
+def test_world1_gather_decode_int8_root_slab_fp32_in_place(hp, dev, comm1):
+    """The int8 wire's gather (hpdct_gather_decode_i8): the
+    root computes its own slab as fp32 in place in the fp32 frame and passes no
+    int8 slab; at world 1 there are no peers, so nothing is received or
+    decoded and the int8 scratch frame is left untouched."""
+    import torch
+    h, w = 1032, 520
+    x = torch.empty((h, w), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=5)
+    frame = torch.empty((h, w), dtype=torch.float32, device=dev)
+    frame8 = torch.full((h, w), 7, dtype=torch.int8, device=dev)
+    hp.forward_slab(comm1, x, frame, h, w)
+    hp.gather_decode_i8(comm1, None, frame8, frame, h, w, root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(frame.view(torch.int32), hp.forward(x).view(torch.int32))
+    assert bool((frame8 == 7).all())
+    # the same through a per-process communicator (its agreement all-reduce first)
+    c = hp.Comm.init_rank(1, hp.comm_unique_id(), 0, dev.index)
+    try:
+        hp.gather_decode_i8(c, None, frame8, frame, h, w, root=0)
+        torch.cuda.synchronize()
+        assert torch.equal(frame.view(torch.int32), hp.forward(x).view(torch.int32))
+    finally:
+        c.destroy()
+
+
+def test_world1_group_posts_queued_gathers_at_group_end(hp, dev, comm1):
+    """init_all communicators inside hpdct_group_start/end: the gathers are
+    queued and posted at hpdct_group_end once the round agrees:
+    two gathers (fp32, then int8) in one group land after the group end."""
+    import torch
+    x = torch.empty((256, 512), dtype=torch.uint8, device=dev)
+    hp.fill_hash_u8(x, seed=17)
+    f32, i8 = hp.forward(x), hp.forward(x, out_dtype=torch.int8)
+    fr32, fr8 = torch.zeros_like(f32), torch.zeros_like(i8)
+    torch.cuda.synchronize()
+    hp.group_start()
+    hp.gather_rows(comm1, f32, fr32, 256, 512, root=0)
+    hp.gather_rows(comm1, i8, fr8, 256, 512, root=0)
+    hp.group_end()
+    torch.cuda.synchronize()
+    assert torch.equal(fr32.view(torch.int32), f32.view(torch.int32)) and torch.equal(fr8, i8)
+
+
+def test_world1_group_with_a_failed_gather_posts_nothing(hp, dev, comm1):
+    """A gather that fails its own checks inside a group fails the whole
+    round: hpdct_group_end posts none of the group's gathers and reports the
+    error (nothing is left waiting on a peer)."""
+    import torch
+    good = torch.full((64, 64), 5.0, dtype=torch.float32, device=dev)
+    frame = torch.zeros_like(good)
+    hp.group_start()
+    hp.gather_rows(comm1, good, frame, 64, 64, root=0)
+    with pytest.raises(hp.HpdctError):
+        hp.gather_rows(comm1, good, frame, 64, 64, root=1)
+    with pytest.raises(hp.HpdctError):
+        hp.group_end()
+    torch.cuda.synchronize()
+    assert bool((frame == 0).all())
+    # the next group starts clean
+    hp.group_start()
+    hp.gather_rows(comm1, good, frame, 64, 64, root=0)
+    hp.group_end()
+    torch.cuda.synchronize()
+    assert torch.equal(frame, good)
+
+
 def test_driver_sharded_mode_one_gpu():
     exe = os.path.join(ROOT, "cuda-dct-idct_amd", "bin", "benchmark_hpdct")
     r = subprocess.run([exe, "4096", "3", "--gpus", "1"], capture_output=True, text=True, timeout=120)
@@ -183,5 +250,8 @@ def test_bench_nccl_process_group_at_world_size_1(tmp_path):
         assert c4[f"predicted_compute_speedup_{k}"] > 0 and line[f"c4_predicted_compute_speedup_{k}"] > 0
     assert c4["gather_bytes_to_root"] == 0 and c4["gather_ms"] < 1.0
     assert c4["end_to_end_ms"] > 0 and c4["end_to_end_int8_ms"] > 0 and c4["decode_int8_ms"] > 0
+    # world 1: the root's slab is fp32 in place for the int8 wire too, nothing is decoded
+    assert c4["decoded_rows_on_root"] == 0 and c4["gather_int8_bytes_to_root"] == 0
+    assert c4["decode_int8_sets"] >= 2
     assert line["parity_spot_check"] is True
     assert line["provenance"]["lib_matches_sources"] is True

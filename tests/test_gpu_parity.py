@@ -602,6 +602,57 @@ def test_quantiser_hardest_tiles(hp, dev, hardest):
     assert bits_equal(to_host(coef), refb)
 
 
+def _retile(strip, tiles_x, tile_rows):
+    """The 8 x 8N strip's tiles laid out row-major into a tile_rows x tiles_x
+    grid of tiles, cycling through them (tiles are position-independent, so
+    the oracle's strip output retiles the same way)."""
+    n = strip.shape[1] // 8
+    t = strip.reshape(8, n, 8).transpose(1, 0, 2)  # (n, 8, 8)
+    idx = np.arange(tile_rows * tiles_x) % n
+    g = t[idx].reshape(tile_rows, tiles_x, 8, 8).transpose(0, 2, 1, 3)
+    return np.ascontiguousarray(g.reshape(tile_rows * 8, tiles_x * 8))
+
+
+@pytest.mark.parametrize("mapping", ["tile", "octet"])
+def test_quantiser_hardest_tiles_forced_mapping(hp, dev, hardest, mapping):
+    """the small hardest-tiles frame under AUTO runs the octet
+    kernels; forced to the tile mapping it runs the uncapped 1024-thread tile
+    kernels with the JPEG forms (fp32 and int8) and the tile round trip."""
+    import torch
+    img, ref = hardest
+    x = to_dev(img, dev)
+    hp.set_mapping(mapping)
+    try:
+        f32 = to_host(hp.forward(x))
+        i8 = to_host(hp.forward(x, out_dtype=torch.int8))
+        coef, _, _ = hp.roundtrip(x, sums=True)
+        coef = to_host(coef)
+    finally:
+        hp.set_mapping("auto")
+    assert bits_equal(f32, ref), mismatches(f32, ref)
+    assert np.array_equal(i8.astype(np.float32), ref)
+    assert bits_equal(coef, ref)
+
+
+@pytest.mark.parametrize("sets_per_cu", [16, 40])
+@pytest.mark.parametrize("tiles_x", [77, 512])
+def test_quantiser_hardest_tiles_mid_big_ragged(hp, dev, hardest, sets_per_cu, tiles_x):
+    """The hardest tiles in frames of 16 sets per CU (the uncapped 1024-thread
+    tile kernel) and 40 (the capped one-wave kernels), at a width of 77 tiles
+    (every 64-tile set straddles two tile rows: kVarStraddle with kVarJpegQ)
+    and of 512 tiles: fp32, int8 and the round trip's coefficients."""
+    import torch
+    img, ref = hardest
+    tile_rows = -(-(sets_per_cu * 256 * 64) // tiles_x)
+    big, refb = _retile(img, tiles_x, tile_rows), _retile(ref, tiles_x, tile_rows)
+    x = to_dev(big, dev)
+    f32 = to_host(hp.forward(x))
+    assert bits_equal(f32, refb), mismatches(f32, refb)
+    assert np.array_equal(to_host(hp.forward(x, out_dtype=torch.int8)).astype(np.float32), refb)
+    coef, _, _ = hp.roundtrip(x, sums=True)
+    assert bits_equal(to_host(coef), refb)
+
+
 # --------------------------------------------------------------------- full-size configs
 def test_c2_1024_bitexact(hp, oracle, dev, golden):
     img = oracle.rand_u8(1024 * 1024).reshape(1024, 1024)

@@ -1,0 +1,223 @@
+// kb_rt.hip -- A/B of the C3 round trip: the tile-per-lane product kernel
+// (hpdct_roundtrip.hpp) against the two-lanes-per-tile kernel
+// (hpdct_rt_duo.hpp) at several register budgets.  One HxW uint8 frame per
+// buffer set, sets rotated (16 sets at 8192^2 = 1 GiB of inputs, 4x the
+// Infinity Cache), interleaved rounds, median of per-batch averages.  Before
+// timing, every variant's coefficients, uint8 reconstruction and sums are
+// compared byte for byte with the product's on two sets.
+//
+//   kb_rt [n=8192 | HxW] [iters=64] [rounds=3] [group=all (= rtduo) | ragged] [sets=16]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "hpdct_rt_duo.hpp"
+
+using namespace hpdct;
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(2);                                                                 \
+        }                                                                            \
+    } while (0)
+
+struct Ctx {
+    TileGrid g;
+    QParams qp;
+    RtSums* sums;  // zeroed by the launcher (memset), as hpdct_roundtrip_u8 did through round 3
+};
+typedef void (*Fn)(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s);
+
+template <bool kStats>
+void tile_rt(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(c.sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, 2, 2, false, 256>), roundtrip_grid(c.g, 256), dim3(256),
+                       0, s, img, coef, static_cast<void*>(recon), kStats ? c.sums : nullptr, c.g, c.qp);
+}
+template <bool kStats, int kQ, int kB, int kW, bool kRun = true>
+void duo_rt(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    if (kStats) (void)hipMemsetAsync(c.sums, 0, sizeof(RtSums), s);
+    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, kQ, kRtReconU8, kRun, kB, kW, 0>), roundtrip_duo_grid(c.g, kB),
+                       dim3(kB), 0, s, img, coef, recon, kStats ? c.sums : nullptr, c.g, c.qp);
+}
+
+// the product candidate: the kernel adds into a zeroed spread slot, the
+// finish kernel folds it over the caller's struct (no memset)
+unsigned long long* g_spread = nullptr;
+template <bool kStats, int kB, int kW, int kSpread, bool kPk = false>
+void duo_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, 2, kRtReconU8, true, kB, kW, kSpread, kPk>), roundtrip_duo_grid(c.g, kB),
+                       dim3(kB), 0, s, img, coef, recon,
+                       reinterpret_cast<RtSums*>(kSpread == -1 || kSpread == -2 ? g_spread + (1u << 18) : g_spread),
+                       c.g, c.qp);
+    if (kSpread > 0 || kSpread == -3 || kSpread == -4) hipLaunchKernelGGL(rt_spread_finish_kernel, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+}
+
+struct V {
+    std::string group, name;
+    Fn fn;
+    bool stats;
+};
+
+template <typename K>
+int vgprs_of(K k) {
+    hipFuncAttributes a{};
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k));
+    return a.numRegs;
+}
+
+int main(int argc, char** argv) {
+    uint64_t H = 8192, W = 8192;
+    if (argc > 1) {
+        const char* x = strchr(argv[1], 'x');
+        if (x) {
+            H = strtoull(argv[1], nullptr, 10), W = strtoull(x + 1, nullptr, 10);
+        } else {
+            H = W = strtoull(argv[1], nullptr, 10);
+        }
+    }
+    const int iters = argc > 2 ? atoi(argv[2]) : 64;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+    const std::string only = argc > 4 ? argv[4] : "all";
+    const uint64_t px = H * W;
+    int nsets = argc > 5 ? atoi(argv[5]) : (int)std::max<uint64_t>(2, (4ull << 28) / px + 1);
+    nsets = std::max(nsets, 2);
+    Ctx c;
+    c.g.tiles_x = (uint32_t)(W / 8), c.g.ntiles = (uint32_t)((H / 8) * (W / 8)), c.g.width = W;
+    for (int i = 0; i < 64; ++i) c.qp.q.v[i] = kDefaultQ.v[i], c.qp.r.v[i] = 1.0f / kDefaultQ.v[i];
+    CK(hipMalloc(&c.sums, sizeof(RtSums)));
+    CK(hipMalloc(&g_spread, 1u << 22));  // spread sub-slots, or one 32-B record per workgroup (-1)
+    CK(hipMemset(g_spread, 0, 1u << 22));
+
+    std::vector<V> vars = {
+        {"rtduo", "tile rt + sums (product)", tile_rt<true>, true},
+        {"rtduo", "duo + sums, w6, spread 64 + finish", duo_sp<true, 256, 6, 64>, true},
+        {"rtduo", "duo + sums, w6, per-wave atomics", duo_sp<true, 256, 6, -3>, true},
+        {"rtduo", "duo + sums, w6, per-wave atomics, DPP sums", duo_sp<true, 256, 6, -4>, true},
+        {"rtduo", "duo + sums, w6, sums not reduced", duo_sp<true, 256, 6, -2>, false},
+        {"rtduo", "duo pk + sums, w6, per-wave atomics, DPP", duo_sp<true, 256, 6, -4, true>, true},
+        {"rtduo", "duo + sums, w6, per-wave DPP, 64-thr WGs", duo_sp<true, 64, 6, -4>, true},
+        {"rtduo", "duo + sums, w6, per-wave DPP, 512-thr WGs", duo_sp<true, 512, 6, -4>, true},
+        {"rtduo", "tile rt no sums", tile_rt<false>, false},
+        {"rtduo", "duo rt no sums, w6", duo_rt<false, 2, 256, 6>, false},
+        {"rtduo", "duo no sums, w6, 64-thr WGs", duo_sp<false, 64, 6, 0>, false},
+        {"rtduo", "tile rt + sums (product) again", tile_rt<true>, true},
+        {"rtduo", "duo + sums, w6, per-wave atomics, DPP again", duo_sp<true, 256, 6, -4>, true},
+        // any width (tiles_x not a multiple of 32): the ragged kernel only
+        {"ragged", "tile rt + sums (product)", tile_rt<true>, true},
+        {"ragged", "duo rt + sums, ragged kernel w5", duo_rt<true, 2, 256, 5, false>, true},
+        {"ragged", "duo rt no sums, ragged kernel w5", duo_rt<false, 2, 256, 5, false>, false},
+        {"ragged", "duo rt + sums, ragged kernel, 6-op quotient", duo_rt<true, 1, 256, 5, false>, true},
+    };
+    vars.erase(std::remove_if(vars.begin(), vars.end(),
+                              [&](const V& v) { return only == "all" ? v.group == "ragged" : v.group != only; }),
+               vars.end());
+    printf("frame %llux%llu, %d sets, VGPRs: tile %d, duo w5 %d w6 %d w7 %d w8 %d, ragged w5 %d\n",
+           (unsigned long long)H, (unsigned long long)W, nsets,
+           vgprs_of(roundtrip_kernel<kRtReconU8, true, 2, 2, false, 256>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 5, 0>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6, 0>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 7, 0>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 8, 0>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, false, 256, 5, 0>));
+
+    std::vector<uint8_t*> img(nsets), rec(nsets);
+    std::vector<float*> coef(nsets);
+    std::vector<uint8_t> h(px);
+    srand(42);
+    for (size_t i = 0; i < px; ++i) h[i] = (uint8_t)(rand() % 256);
+    for (int s = 0; s < nsets; ++s) {
+        CK(hipMalloc(&img[s], px));
+        CK(hipMalloc(&rec[s], px));
+        CK(hipMalloc(&coef[s], px * 4));
+        if (s == 0) {
+            CK(hipMemcpy(img[s], h.data(), px, hipMemcpyHostToDevice));
+        } else {
+            const uint64_t lanes = (px + 15) / 16;
+            hipLaunchKernelGGL(fill_hash_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, 0, img[s], px,
+                               1000ull + s, 0ull);
+        }
+    }
+    CK(hipDeviceSynchronize());
+
+    // correctness: coefficients, reconstruction and sums == the product's, sets 0 and 1
+    {
+        std::vector<float> c0(px), c1(px);
+        std::vector<uint8_t> r0(px), r1(px);
+        for (int s = 0; s < 2; ++s) {
+            RtSums s0{}, s1{};
+            tile_rt<true>(img[s], coef[2], rec[2], c, 0);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(c0.data(), coef[2], px * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(r0.data(), rec[2], px, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&s0, c.sums, sizeof(s0), hipMemcpyDeviceToHost));
+            for (auto& v : vars) {
+                CK(hipMemset(coef[2], 0xa5, px * 4));
+                CK(hipMemset(rec[2], 0x5a, px));
+                CK(hipMemset(c.sums, 0xee, sizeof(RtSums)));
+                v.fn(img[s], coef[2], rec[2], c, 0);
+                const hipError_t le = hipGetLastError();
+                if (le != hipSuccess) {
+                    printf("check %-40s LAUNCH FAILED: %s\n", v.name.c_str(), hipGetErrorString(le));
+                    return 1;
+                }
+                CK(hipDeviceSynchronize());
+                CK(hipMemcpy(c1.data(), coef[2], px * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(r1.data(), rec[2], px, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(&s1, c.sums, sizeof(s1), hipMemcpyDeviceToHost));
+                size_t bc = 0, br = 0;
+                for (size_t i = 0; i < px; ++i) bc += memcmp(&c0[i], &c1[i], 4) != 0, br += r0[i] != r1[i];
+                const bool sok = !v.stats || memcmp(&s0, &s1, sizeof(s0)) == 0;
+                printf("check set %d %-40s coef %s recon %s sums %s\n", s, v.name.c_str(),
+                       bc ? "MISMATCH" : "bit-exact", br ? "MISMATCH" : "bit-exact",
+                       v.stats ? (sok ? "identical" : "DIFFER") : "-");
+                if (bc || br || !sok) {
+                    printf("  %zu coefficients, %zu pixels differ; sums %llu %llu %llu vs %llu %llu %llu\n", bc, br,
+                           s0.sse_f32_fx, s0.sse_u8, s0.sum_x2, s1.sse_f32_fx, s1.sse_u8, s1.sum_x2);
+                    for (size_t i = 0, n = 0; i < px && n < 8; ++i)
+                        if (memcmp(&c0[i], &c1[i], 4) != 0 || r0[i] != r1[i]) {
+                            printf("  px %zu (row %zu col %zu): coef %g vs %g, recon %u vs %u\n", i, i / W, i % W,
+                                   c0[i], c1[i], r0[i], r1[i]);
+                            ++n;
+                        }
+                    return 1;
+                }
+            }
+        }
+    }
+
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<std::vector<float>> us(vars.size());
+    for (int r = 0; r < rounds; ++r) {
+        for (size_t v = 0; v < vars.size(); ++v) {
+            for (int w = 0; w < 2 * nsets; ++w) vars[v].fn(img[w % nsets], coef[w % nsets], rec[w % nsets], c, 0);
+            for (int i = 0; i < iters; i += nsets) {
+                CK(hipEventRecord(a, 0));
+                for (int k = 0; k < nsets; ++k) vars[v].fn(img[k], coef[k], rec[k], c, 0);
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, a, b));
+                us[v].push_back(ms * 1e3f / nsets);
+            }
+        }
+    }
+    printf("%-42s %10s %10s %8s\n", "variant", "median_us", "min_us", "frac8T");
+    for (size_t v = 0; v < vars.size(); ++v) {
+        auto t = us[v];
+        std::sort(t.begin(), t.end());
+        const double med = t[t.size() / 2];
+        printf("%-42s %10.2f %10.2f %8.3f\n", vars[v].name.c_str(), med, t[0], 6.0 * px / (med * 1e-6) / 8e12);
+    }
+    return 0;
+}
