@@ -55,14 +55,32 @@ struct RtSums {
     unsigned long long sum_x2;      // sum x^2, exact
 };
 enum : int { kRtReconNone = 0, kRtReconU8 = 1, kRtReconF32 = 2 };
-// fast: integer table in 1..255 with int8-range quotients (verified quotient,
-// packed int8 rows); sums may be nullptr (no statistics), recon nullptr with
-// kRtReconNone.
-// zero_sums: the launch overwrites *sums (the kernel adds into a library slot
-// kept per sums pointer, a one-wave kernel moves it over *sums; a memset of
-// *sums before the kernel when no slot can be had); false: adds into *sums
+// fast: integer table in 1..255 with int8-range quotients (verified quotient);
+// sums may be nullptr (no statistics), recon nullptr with kRtReconNone.
+// zero_sums: the launch overwrites *sums, else adds to it.  The kernel adds
+// into a library spread slot kept per sums pointer and a one-wave kernel folds
+// it into *sums (a memset of *sums and the tile kernel when no slot can be had).
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s);
+// The pieces launch_roundtrip (hpdct_roundtrip.hip) chooses from:
+//  - the tile-per-lane kernels, one unit per reconstruction kind
+//    (hpdct_rt_tile_{u8,f32,none}.hip); sums: the struct (or spread
+//    sub-slot 0) the workgroups add into, or nullptr;
+//  - the two-lanes-per-tile kernel (hpdct_rt_duo.hip): fast 1 or 2, a uint8
+//    reconstruction (recon) or none (nullptr); spread: a zeroed spread slot
+//    (kRtSpread sub-slots, hpdct_roundtrip.hpp) the waves add into, or
+//    nullptr for no sums;
+//  - the finish kernel folding a spread slot into *dst (overwrite, or add
+//    when accumulate) and zeroing it.
+hipError_t launch_rt_tile_u8(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g,
+                             const QParams& qp, int fast, hipStream_t s);
+hipError_t launch_rt_tile_f32(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g,
+                              const QParams& qp, int fast, hipStream_t s);
+hipError_t launch_rt_tile_none(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g,
+                               const QParams& qp, int fast, hipStream_t s);
+hipError_t launch_rt_duo(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread,
+                         const TileGrid& g, const QParams& qp, int fast, hipStream_t s);
+hipError_t launch_rt_finish(RtSums* dst, unsigned long long* spread, bool accumulate, hipStream_t s);
 
 // A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch
 // device pointer pairs travel in the kernel arguments (1 KiB).

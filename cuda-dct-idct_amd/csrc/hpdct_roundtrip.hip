@@ -1,26 +1,30 @@
-// hpdct_roundtrip.hip -- launcher of the one-pass round trip (hpdct_roundtrip.hpp).
+// hpdct_roundtrip.hip -- launcher of the one-pass round trip: which kernel
+// (the two-lanes-per-tile kernel of hpdct_rt_duo.hpp, or the tile-per-lane
+// kernel of hpdct_roundtrip.hpp) and where its quality sums go.
 #include <map>
 #include <mutex>
 
+#include "hpdct.h"
 #include "hpdct_roundtrip.hpp"
 
 namespace hpdct {
 namespace {
 
-// Sums slots for hpdct_roundtrip_u8, one per (device, caller's sums pointer),
-// handed out from zeroed chunks and never returned: the round trip adds into
-// the slot and rt_finish_kernel moves it over the caller's struct, leaving it
-// zero for the next launch with that pointer.  Launches with one sums pointer
-// are ordered (one stream, or one graph) or race on the caller's struct
-// anyway, so they may share its slot.  nullptr (the launch then zeroes the
-// caller's struct with a memset) when a new chunk would be needed inside a
-// stream capture, or past kMaxSlots pointers on a device.
-constexpr size_t kSlotChunk = 1024;
-constexpr size_t kMaxSlots = size_t(1) << 16;
+// Spread slots for the sums (kRtSpread sub-slots, kRtSpreadBytes each), one
+// per (device, caller's sums pointer), handed out from zeroed chunks and never
+// returned: the round trip adds into the slot and rt_spread_finish_kernel
+// folds it into the caller's struct, leaving it zero for the next launch with
+// that pointer.  Launches with one sums pointer are ordered (one stream, or
+// one graph) or race on the caller's struct anyway, so they may share its
+// slot.  nullptr when a new chunk would be needed inside a stream capture, or
+// past kMaxSlots pointers on a device: the launch then takes the tile kernel
+// with a memset of *sums (overwrite) or atomics into *sums (accumulate).
+constexpr size_t kSlotChunk = 256;  // 256 x 16 KiB = 4 MiB per allocation
+constexpr size_t kMaxSlots = size_t(1) << 14;
 
 struct DeviceSlots {
-    std::map<const void*, RtSums*> by_sums;
-    RtSums* chunk = nullptr;
+    std::map<const void*, unsigned long long*> by_sums;
+    unsigned char* chunk = nullptr;
     size_t used = kSlotChunk;
     hipStream_t zero_stream = nullptr;
 };
@@ -28,7 +32,7 @@ struct DeviceSlots {
 std::mutex g_slot_mutex;
 std::map<int, DeviceSlots> g_slots;
 
-RtSums* slot_for(int dev, const void* sums, hipStream_t s) {
+unsigned long long* slot_for(int dev, const void* sums, hipStream_t s) {
     std::lock_guard<std::mutex> lock(g_slot_mutex);
     DeviceSlots& d = g_slots[dev];
     auto it = d.by_sums.find(sums);
@@ -51,17 +55,17 @@ RtSums* slot_for(int dev, const void* sums, hipStream_t s) {
             return nullptr;
         }
         void* p = nullptr;
-        if (hipMalloc(&p, kSlotChunk * sizeof(RtSums)) != hipSuccess) return nullptr;
+        if (hipMalloc(&p, kSlotChunk * kRtSpreadBytes) != hipSuccess) return nullptr;
         // zero before any stream can launch with one of its slots
-        if (hipMemsetAsync(p, 0, kSlotChunk * sizeof(RtSums), d.zero_stream) != hipSuccess ||
+        if (hipMemsetAsync(p, 0, kSlotChunk * kRtSpreadBytes, d.zero_stream) != hipSuccess ||
             hipStreamSynchronize(d.zero_stream) != hipSuccess) {
             (void)hipFree(p);
             return nullptr;
         }
-        d.chunk = static_cast<RtSums*>(p);
+        d.chunk = static_cast<unsigned char*>(p);
         d.used = 0;
     }
-    RtSums* const slot = d.chunk + d.used++;
+    auto* const slot = reinterpret_cast<unsigned long long*>(d.chunk + d.used++ * kRtSpreadBytes);
     d.by_sums.emplace(sums, slot);
     return slot;
 }
@@ -70,20 +74,53 @@ RtSums* slot_for(int dev, const void* sums, hipStream_t s) {
 // non-zero.  The slot is zeroed behind it on the same stream, so the pointer
 // keeps its slot (a graph captured earlier with that slot stays correct);
 // only when even that fails does the pointer get a fresh slot next time.
-void recover_slot(int dev, const void* sums, RtSums* slot, hipStream_t s) {
-    if (hipMemsetAsync(slot, 0, sizeof(RtSums), s) == hipSuccess) return;
+void recover_slot(int dev, const void* sums, unsigned long long* slot, hipStream_t s) {
+    if (hipMemsetAsync(slot, 0, kRtSpreadBytes, s) == hipSuccess) return;
     std::lock_guard<std::mutex> lock(g_slot_mutex);
     g_slots[dev].by_sums.erase(sums);
 }
 
+hipError_t tile(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums, const TileGrid& g,
+                const QParams& qp, int fast, hipStream_t s) {
+    switch (recon_kind) {
+        case kRtReconU8: return launch_rt_tile_u8(img, coef, recon, sums, g, qp, fast, s);
+        case kRtReconF32: return launch_rt_tile_f32(img, coef, recon, sums, g, qp, fast, s);
+        default: return launch_rt_tile_none(img, coef, nullptr, sums, g, qp, fast, s);
+    }
+}
+
 }  // namespace
 
+// The kernel: the two-lanes-per-tile round trip (hpdct_rt_duo.hpp) for the
+// verified quotient (fast 1 or 2) with a uint8 reconstruction or none, when
+// its sums (if any) have a spread slot, the width is a multiple of 256
+// pixels (whole 32-tile runs per wave) and the mapping is not forced to
+// "tile"; 8192^2 with sums 76.3-76.7 us against 79.7 for the tile kernel with
+// the same sums path and 82.4 with round 4's memset, without sums 67.0
+// against 76.8 (tools/kb_rt, profiles/r05/b/).  Otherwise the tile-per-lane
+// kernel (fp32 reconstruction, IEEE division, ragged widths, forced tile
+// mapping), with its sums in the spread slot's sub-slot 0 when it has one.
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s) {
     int dev = -1;
-    RtSums* slot = nullptr;
-    if (sums && zero_sums && hipGetDevice(&dev) == hipSuccess) slot = slot_for(dev, sums, s);
-    const hipError_t e = launch_roundtrip_impl(img, coef, recon, recon_kind, sums, g, qp, fast, s, zero_sums, slot);
+    unsigned long long* slot = nullptr;
+    if (sums && hipGetDevice(&dev) == hipSuccess) slot = slot_for(dev, sums, s);
+    const bool duo = fast != 0 && recon_kind != kRtReconF32 && (!sums || slot) && g.tiles_x % 32u == 0u &&
+                     mapping_mode() != HPDCT_MAPPING_TILE;
+    hipError_t e;
+    if (duo) {
+        e = launch_rt_duo(img, coef, recon_kind == kRtReconU8 ? static_cast<uint8_t*>(recon) : nullptr, slot, g, qp,
+                          fast, s);
+    } else if (slot) {
+        e = tile(img, coef, recon, recon_kind, reinterpret_cast<RtSums*>(slot), g, qp, fast, s);
+    } else {
+        if (sums && zero_sums) {
+            e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);
+            if (e != hipSuccess) return e;
+        }
+        return tile(img, coef, recon, recon_kind, sums, g, qp, fast, s);
+    }
+    if (e == hipSuccess && slot) e = launch_rt_finish(sums, slot, !zero_sums, s);
     if (e != hipSuccess && slot) recover_slot(dev, sums, slot, s);
     return e;
 }

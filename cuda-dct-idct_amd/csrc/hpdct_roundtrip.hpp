@@ -18,15 +18,19 @@
 // Quality sums (kStats), per frame, as hpdct_quality.py defines them:
 //   sum_x2  = sum x^2                       exact: v_dot4_u32_u8 on the packed
 //   sse_u8  = sum (x - u8(R+128))^2        pixel bytes (x.x, x.r8, r8.r8), uint64
-//   sse_f32 = sum (x - (R+128))^2          per tile an fp32 fma chain over the 64
-//             pixels, rounded to a multiple of 2^-16 and added as uint64: the
-//             result does not depend on the order tiles finish in, but it is
-//             not the exact sum (each tile's fp32 chain rounds; relative error
-//             ~1e-9 at 8192^2, tests/test_gpu_roundtrip.py)
+//   sse_f32 = sum (x - (R+128))^2          per tile FOUR fp32 fma chains, one per
+//             (row parity, column parity) class of its pixels, each in row-major
+//             order from +0, each rounded to a multiple of 2^-16 (rt_sse_fix)
+//             and added as uint64: the result does not depend on the order tiles
+//             finish in, but it is not the exact sum (relative error ~1e-10 at
+//             8192^2, tests/test_gpu_roundtrip.py).  Four classes since round 5:
+//             the two-lanes-per-tile kernel (hpdct_rt_duo.hpp) holds the rows of
+//             one parity per lane and the columns of one parity per half of a
+//             packed register, so its chains need no cross-lane hand-off; this
+//             kernel keeps the same four chains, so both give the same sums.
 // Workgroup partials are added with one 64-bit atomic per field per workgroup,
-// into the caller's struct (hpdct_roundtrip_u8_accumulate) or into a library
-// slot that rt_finish_kernel then copies over the caller's struct and zeroes
-// (hpdct_roundtrip_u8).
+// into the caller's struct or sub-slot 0 of a library spread slot that
+// rt_spread_finish_kernel then folds into the caller's struct.
 #pragma once
 
 #include "hpdct_kernels_impl.hpp"
@@ -38,6 +42,24 @@ constexpr float kRtFixScale = 65536.0f;  // sse_f32 fixed point: 2^-16
 // field then holds no sum; include/hpdct.h HPDCT_SSE_F32_INVALID)
 constexpr unsigned long long kRtSseF32Invalid = 1ull << 63;
 
+// sse_f32 of one fp32 chain in fixed point (units 2^-16): ok stays true when
+// the chain is finite and below 2^24 (fixed point below 2^40), otherwise the
+// chain adds nothing and ok turns false (the caller then sets
+// kRtSseF32Invalid, so the field can neither wrap nor read as a small value).
+__device__ __forceinline__ unsigned long long rt_sse_fix(float chain, bool& ok) {
+    const float fx = __builtin_rintf(chain * kRtFixScale);
+    const bool good = fx < 0x1p40f;  // false for NaN
+    ok = ok && good;
+    return good ? static_cast<unsigned long long>(fx) : 0ull;
+}
+
+// The spread slot of the sums (round 5): kRtSpread sub-slots of 3 x uint64,
+// kRtSpreadStride words (256 B) apart, so that the atomics of many waves land
+// on kRtSpread different lines; rt_spread_finish_kernel folds them.
+constexpr int kRtSpread = 64;
+constexpr uint32_t kRtSpreadStride = 32;
+constexpr size_t kRtSpreadBytes = kRtSpread * kRtSpreadStride * sizeof(unsigned long long);
+
 namespace {
 
 // unpack int8 byte k of w into an exact float (sign-extending byte convert)
@@ -48,6 +70,41 @@ __device__ __forceinline__ float i8_byte_f32(uint32_t w, int k) {
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     unroll<6>([&](auto s) { v += __shfl_xor(v, 1 << s, 64); });
     return v;
+}
+
+// Sum over the wave in DPP steps (row_shr 1, 2, 4, 8 inside each 16-lane row,
+// then row_bcast 15 and 31 across rows): lane 63 ends with the total, read
+// back with one readlane.  No LDS traffic, unlike __shfl_xor.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), kCtrl, kRowMask, 0xf, false));
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void dpp_add(uint32_t& v) {
+    v += dpp_u32<kCtrl, kRowMask>(v);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void dpp_add(unsigned long long& v) {
+    const uint32_t lo = dpp_u32<kCtrl, kRowMask>(static_cast<uint32_t>(v));
+    const uint32_t hi = dpp_u32<kCtrl, kRowMask>(static_cast<uint32_t>(v >> 32));
+    v += (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+template <typename U>
+__device__ __forceinline__ U wave_sum_dpp(U v) {
+    dpp_add<0x111, 0xf>(v);  // row_shr:1
+    dpp_add<0x112, 0xf>(v);  // row_shr:2
+    dpp_add<0x114, 0xf>(v);  // row_shr:4
+    dpp_add<0x118, 0xf>(v);  // row_shr:8
+    dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    if constexpr (sizeof(U) == 8) {
+        const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v)), 63));
+        const uint32_t hi =
+            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v >> 32)), 63));
+        return (static_cast<unsigned long long>(hi) << 32) | lo;
+    } else {
+        return static_cast<U>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+    }
 }
 
 }  // namespace
@@ -99,7 +156,7 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, float> coef_sink{coef, g.width, slots};
     const RowSink<kVar, float> rf32_sink{static_cast<float*>(recon), g.width, slots};
-    float acc_f = 0.0f;                          // this lane's tile: sum (x - (R+128))^2
+    float acc_f[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};  // this lane's tile: the four sse_f32 chains
     uint32_t acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;  // sum x^2, x.r8, r8^2 (<= 64 * 255^2)
 
     uint2* stash = nullptr;  // kRaw == 2: this wave's [row][lane] pixel words
@@ -174,7 +231,7 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
                 acc_rr = __builtin_amdgcn_udot4(r8.y, r8.y, acc_rr, false);
                 unroll<8>([&](auto u) {
                     const float e = byte_f32(u < 4 ? w.x : w.y, u & 3) - r[u];
-                    acc_f = __builtin_fmaf(e, e, acc_f);
+                    acc_f[v & 1][u & 1] = __builtin_fmaf(e, e, acc_f[v & 1][u & 1]);
                 });
             }
             if constexpr (kRecon == kRtReconU8) {
@@ -194,18 +251,16 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
 
     if constexpr (kStats) {
         // lanes without a tile (ragged last set, or waves past the end) hold zeros.
-        // A tile's fixed-point sse_f32 below 2^40 (sse < 2^24, i.e. a mean
-        // |x - R| under 512 per pixel) is added exactly; a larger or non-finite
-        // one (IEEE path with an extreme table) adds nothing and sets the
-        // sticky bit 63 of the field instead (kRtSseF32Invalid): the sum can
-        // then neither wrap nor read as a small value
-        const float fx = __builtin_rintf(acc_f * kRtFixScale);
-        const bool f_ok = fx < 0x1p40f;  // false for NaN
-        unsigned long long f = f_ok ? static_cast<unsigned long long>(fx) : 0ull;
+        // A chain's fixed point below 2^40 (sse < 2^24) is added exactly; a
+        // larger or non-finite one (IEEE path with an extreme table) adds
+        // nothing and sets the sticky bit 63 of the field (rt_sse_fix)
+        bool f_ok = true;
+        unsigned long long f = rt_sse_fix(acc_f[0][0], f_ok) + rt_sse_fix(acc_f[0][1], f_ok) +
+                               rt_sse_fix(acc_f[1][0], f_ok) + rt_sse_fix(acc_f[1][1], f_ok);
         unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
         unsigned long long xx = static_cast<unsigned long long>(acc_xx);
         f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
-        // a wave's f is < 64 * 2^40: bit 63 of its slot carries the wave's flag
+        // a wave's f is < 64 * 4 * 2^40: bit 63 of its slot carries the wave's flag
         if (__builtin_amdgcn_ballot_w64(!f_ok) != 0) f |= kRtSseF32Invalid;
         __shared__ unsigned long long part[kBlock / 64][3];
         const uint32_t w = threadIdx.x / 64u;
@@ -224,17 +279,35 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
     }
 }
 
-// hpdct_roundtrip_u8's sums: the round trip adds into a library slot (all
-// zero between launches); this one-wave kernel, next on the stream, writes
-// the slot over the caller's struct and zeroes it.  8192^2: 77.6 us per
-// launch against 79.3 with a memset of the caller's struct before the kernel
-// and 76.6 with no zeroing at all (profiles/r04/j/kb3_rtring_8192.log).
-__global__ __launch_bounds__(64) void rt_finish_kernel(RtSums* __restrict__ dst, RtSums* __restrict__ slot) {
-    if (threadIdx.x < 3u) {
-        unsigned long long* const src = reinterpret_cast<unsigned long long*>(slot) + threadIdx.x;
-        reinterpret_cast<unsigned long long*>(dst)[threadIdx.x] = *src;
-        *src = 0ull;
+// Folds the kRtSpread sub-slots of a spread slot into *dst (overwriting it,
+// or adding to it when accumulate) and zeroes them: one wave, lane i reads
+// sub-slot i.  Next on the stream after a round trip that added into the slot
+// (hpdct_roundtrip_u8 and _accumulate, round 5).  The one-wave kernel costs
+// less than the memset it replaced (round 4: 77.6 us per 8192^2 launch against
+// 79.3 with a memset of the caller's struct before the kernel,
+// profiles/r04/j/kb3_rtring_8192.log).
+template <int kN = kRtSpread>
+__global__ __launch_bounds__(64) void rt_spread_finish_kernel(RtSums* __restrict__ dst,
+                                                              unsigned long long* __restrict__ slot, int accumulate) {
+    const uint32_t l = threadIdx.x;
+    unsigned long long v[3] = {0ull, 0ull, 0ull}, bad[3] = {0ull, 0ull, 0ull};
+    for (uint32_t k = l; k < static_cast<uint32_t>(kN); k += 64u) {
+        unroll<3>([&](auto f) {
+            const unsigned long long x = slot[k * kRtSpreadStride + f];
+            v[f] += x & ~kRtSseF32Invalid, bad[f] |= x & kRtSseF32Invalid;
+            slot[k * kRtSpreadStride + f] = 0ull;
+        });
     }
+    unroll<3>([&](auto f) {
+        const unsigned long long sum = wave_sum_dpp(v[f]);
+        const bool flagged = __builtin_amdgcn_ballot_w64(bad[f] != 0ull) != 0ull;
+        if (l == 0u) {
+            auto* const d = reinterpret_cast<unsigned long long*>(dst) + f;
+            unsigned long long out = accumulate ? *d + sum : sum;
+            if (flagged) out |= kRtSseF32Invalid;
+            *d = out;
+        }
+    });
 }
 
 inline dim3 roundtrip_grid(const TileGrid& g, uint32_t block = kRtBlock) {
@@ -273,33 +346,5 @@ hipError_t go_r(const uint8_t* img, float* coef, void* recon, RtSums* sums, cons
     return go_q<kRecon, false>(img, coef, recon, sums, g, qp, qmode, s);
 }
 }  // namespace rt_detail
-
-// fast: 0 IEEE division, 1 the verified 3-op quotient, 2 with the default
-// JPEG table's per-position forms (hpdct_kernels.h launch_roundtrip).
-// Sums: zero_sums false adds into *sums; else with a slot (all zero, kept for
-// this sums pointer by the caller of this function) the kernel adds into the
-// slot and rt_finish_kernel moves it over *sums, and without one a memset
-// zeroes *sums before the kernel.  A template, so that a translation unit
-// including this header for the kernels alone does not instantiate (and
-// compile) every round-trip variant.
-template <int = 0>
-hipError_t launch_roundtrip_impl(const uint8_t* img, float* coef, void* recon, int recon_kind,
-                                        RtSums* sums, const TileGrid& g, const QParams& qp, int fast,
-                                        hipStream_t s, bool zero_sums = true, RtSums* slot = nullptr) {
-    RtSums* const acc = sums && zero_sums && slot ? slot : sums;
-    if (sums && zero_sums && !slot) {
-        const hipError_t e = hipMemsetAsync(sums, 0, sizeof(RtSums), s);
-        if (e != hipSuccess) return e;
-    }
-    hipError_t e;
-    switch (recon_kind) {
-        case kRtReconU8: e = rt_detail::go_r<kRtReconU8>(img, coef, recon, acc, g, qp, fast, s); break;
-        case kRtReconF32: e = rt_detail::go_r<kRtReconF32>(img, coef, recon, acc, g, qp, fast, s); break;
-        default: e = rt_detail::go_r<kRtReconNone>(img, coef, nullptr, acc, g, qp, fast, s); break;
-    }
-    if (e != hipSuccess || acc == sums) return e;
-    hipLaunchKernelGGL(rt_finish_kernel, dim3(1), dim3(64), 0, s, sums, slot);
-    return hipGetLastError();
-}
 
 }  // namespace hpdct

@@ -80,41 +80,6 @@ __device__ __forceinline__ float px_minus128(uint32_t w_xor, int k) {
     return static_cast<float>(static_cast<int32_t>(static_cast<int8_t>(w_xor >> (8 * k))));
 }
 
-// Sum over the wave in DPP steps (row_shr 1, 2, 4, 8 inside each 16-lane row,
-// then row_bcast 15 and 31 across rows): lane 63 ends with the total, read
-// back with one readlane.  No LDS traffic, unlike __shfl_xor.
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), kCtrl, kRowMask, 0xf, false));
-}
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void dpp_add(uint32_t& v) {
-    v += dpp_u32<kCtrl, kRowMask>(v);
-}
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void dpp_add(unsigned long long& v) {
-    const uint32_t lo = dpp_u32<kCtrl, kRowMask>(static_cast<uint32_t>(v));
-    const uint32_t hi = dpp_u32<kCtrl, kRowMask>(static_cast<uint32_t>(v >> 32));
-    v += (static_cast<unsigned long long>(hi) << 32) | lo;
-}
-template <typename U>
-__device__ __forceinline__ U wave_sum_dpp(U v) {
-    dpp_add<0x111, 0xf>(v);  // row_shr:1
-    dpp_add<0x112, 0xf>(v);  // row_shr:2
-    dpp_add<0x114, 0xf>(v);  // row_shr:4
-    dpp_add<0x118, 0xf>(v);  // row_shr:8
-    dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
-    dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
-    if constexpr (sizeof(U) == 8) {
-        const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v)), 63));
-        const uint32_t hi =
-            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v >> 32)), 63));
-        return (static_cast<unsigned long long>(hi) << 32) | lo;
-    } else {
-        return static_cast<U>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
-    }
-}
-
 // Where a duo wave's rows live: the wave's first tile's top-left pixel (a
 // wave-uniform base, SGPRs) plus a 32-bit per-lane offset.  A wave's 32 tiles
 // are consecutive in row-major tile order, so every offset is >= 0 (tiles in
@@ -131,6 +96,29 @@ struct DuoAddr {
 
 }  // namespace
 
+// The quality sums of one reconstructed row (8 pixels) of a lane: the exact
+// integer sums on the packed bytes (v_dot4_u32_u8: x.x, x.r8, r8.r8) and the
+// row's terms of the lane's two sse_f32 chains, (x - r)^2 for the even
+// columns into acc_f2.x and the odd ones into acc_f2.y, in column order (one
+// v_pk_add_f32 and one v_pk_fma_f32 per column pair).  With the rows a lane
+// owns (2k + h, in order), its two chains are the (row parity h, column
+// parity) classes of the tile's sse_f32 definition (hpdct_roundtrip.hpp).
+__device__ __forceinline__ void rt_duo_row_sums(uint2 w, const float (&r)[8], uint2 r8, f32x2& acc_f2,
+                                                uint32_t& acc_xx, uint32_t& acc_xr, uint32_t& acc_rr) {
+    acc_xx = __builtin_amdgcn_udot4(w.x, w.x, acc_xx, false);
+    acc_xx = __builtin_amdgcn_udot4(w.y, w.y, acc_xx, false);
+    acc_xr = __builtin_amdgcn_udot4(w.x, r8.x, acc_xr, false);
+    acc_xr = __builtin_amdgcn_udot4(w.y, r8.y, acc_xr, false);
+    acc_rr = __builtin_amdgcn_udot4(r8.x, r8.x, acc_rr, false);
+    acc_rr = __builtin_amdgcn_udot4(r8.y, r8.y, acc_rr, false);
+    unroll<4>([&](auto j) {
+        const uint32_t word = j < 2 ? w.x : w.y;
+        const f32x2 x2 = {byte_f32(word, (2 * j) & 3), byte_f32(word, (2 * j + 1) & 3)};
+        const f32x2 e2 = x2 - f32x2{r[2 * j], r[2 * j + 1]};
+        acc_f2 = fma2(e2, e2, acc_f2);
+    });
+}
+
 // One wave's 32 tiles (kQMode, kRecon: as roundtrip_duo_kernel).  kRun:
 // every wave's 32 tiles are one run of a tile row (tiles_x a multiple of 32),
 // all valid; the coefficient rows are re-staged for 1 KiB-contiguous stores.
@@ -140,7 +128,7 @@ struct DuoAddr {
 template <bool kStats, int kQMode, int kRecon, bool kRun>
 __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, float* __restrict__ coef,
                                             uint8_t* __restrict__ recon, const DuoAddr& a, uint32_t h,
-                                            const float (&tab)[2][64], float4* __restrict__ slots, float& acc_f,
+                                            const float (&tab)[2][64], float4* __restrict__ slots, f32x2& acc_f2,
                                             uint32_t& acc_xx, uint32_t& acc_xr, uint32_t& acc_rr) {
     constexpr bool kNT = true;
     const TSource<true, true> T(nullptr);  // built-in T, zero terms skipped (finite operands)
@@ -247,7 +235,6 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
     });
     unroll<4>([&](auto k) { unroll<4>([&](auto c) { xswap(pa[k][c], pb[k][c]); }); });
     // ---- inverse pass 2: R[v][u] = chain_i P[v][i] T[i][u], + 128, uint8, sums
-    float chain = 0.0f;  // lanes 0..31: the tile's sse_f32 chain so far (rows < 2k)
     unroll<4>([&](auto k) {
         const float prow[8] = {pa[k][0], pa[k][1], pa[k][2], pa[k][3], pb[k][0], pb[k][1], pb[k][2], pb[k][3]};
         float r[8];
@@ -257,36 +244,13 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
             r[u] = s + 128.0f;  // add_matrix_scalar (utils_kernels.cu:29)
         });
         const uint2 r8 = make_uint2(pack_u8x4(r[0], r[1], r[2], r[3]), pack_u8x4(r[4], r[5], r[6], r[7]));
-        if constexpr (kStats) {
-            const uint2 w = raw[k];
-            acc_xx = __builtin_amdgcn_udot4(w.x, w.x, acc_xx, false);
-            acc_xx = __builtin_amdgcn_udot4(w.y, w.y, acc_xx, false);
-            acc_xr = __builtin_amdgcn_udot4(w.x, r8.x, acc_xr, false);
-            acc_xr = __builtin_amdgcn_udot4(w.y, r8.y, acc_xr, false);
-            acc_rr = __builtin_amdgcn_udot4(r8.x, r8.x, acc_rr, false);
-            acc_rr = __builtin_amdgcn_udot4(r8.y, r8.y, acc_rr, false);
-            float e[8];
-            unroll<8>([&](auto u) { e[u] = byte_f32(u < 4 ? w.x : w.y, u & 3) - r[u]; });
-            // row 2k continues the chain in lanes 0..31; its sum moves to
-            // lanes 32..63 for row 2k+1, whose sum comes back for row 2k+2
-            float s = chain;
-            unroll<8>([&](auto u) { s = __builtin_fmaf(e[u], e[u], s); });
-            float to_hi = s, keep = s;
-            xswap(to_hi, keep);  // lanes 32..63: to_hi = lane - 32's s
-            float s2 = to_hi;
-            unroll<8>([&](auto u) { s2 = __builtin_fmaf(e[u], e[u], s2); });
-            float back = s2, to_lo = s2;
-            xswap(back, to_lo);  // lanes 0..31: to_lo = lane + 32's s2
-            chain = to_lo;
-        }
+        if constexpr (kStats) rt_duo_row_sums(raw[k], r, r8, acc_f2, acc_xx, acc_xr, acc_rr);
         if constexpr (kRecon == kRtReconU8) {
             if (kRun || a.valid) st<kNT>(reinterpret_cast<uint2*>(recon + a.base + a.off(2u * k + h)), r8);
         }
     });
     if constexpr (kStats) {
-        // lanes 0..31 hold the tile's full chain; a tile is counted once
-        acc_f = (h == 0u && (kRun || a.valid)) ? chain : 0.0f;
-        if (!(kRun || a.valid)) acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
+        if (!(kRun || a.valid)) acc_f2 = f32x2{0.0f, 0.0f}, acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
     }
 }
 
@@ -294,208 +258,21 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
 // table's short forms where both of an instruction's positions have one.
 // kRecon: kRtReconU8 or kRtReconNone.  kWaves: waves per SIMD the register
 // allocation must allow.
-// The same round trip with both transforms, the quantiser, the dequantiser
-// and the level shift in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 /
-// v_pk_add_f32: two IEEE operations per instruction, each half rounded as
-// the scalar one, so bit-identical).  Pass 1 of each transform pairs two
-// columns of the lane's half (same T entry, broadcast); pass 2 pairs output
-// columns (u, u+1) (T entries differ per half; a term whose T entry is zero
-// in one half only adds fma(0, P, s) = s exactly: P is finite and a chain
-// from +0 never holds -0).  The quantiser takes a column pair in one packed
-// sequence: the short JPEG form when all four positions of the pair (two
-// rows, the lanes' 2k and 2k+1, times two columns) have one, the verified
-// 6-op quotient otherwise.
-template <bool kStats, int kQMode, int kRecon, bool kRun>
-__device__ __forceinline__ void rt_duo_body_pk(const uint8_t* __restrict__ img, float* __restrict__ coef,
-                                               uint8_t* __restrict__ recon, const DuoAddr& a, uint32_t h,
-                                               const float (&tab)[2][64], float4* __restrict__ slots, float& acc_f,
-                                               uint32_t& acc_xx, uint32_t& acc_xr, uint32_t& acc_rr) {
-    constexpr bool kNT = true;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint8_t* const src = img + a.base;
-    auto T = [](int v, int i) constexpr { return kBuiltinT.v[v * 8 + i]; };
-
-    uint2 raw[4];
-    unroll<4>([&](auto k) {
-        raw[k] = make_uint2(0u, 0u);
-        if (kRun || a.valid) raw[k] = *reinterpret_cast<const uint2*>(src + a.off(2u * k + h));
-    });
-    uint32_t lo[4], hi[4];
-    unroll<4>([&](auto k) {
-        lo[k] = raw[k].x ^ 0x80808080u, hi[k] = raw[k].y ^ 0x80808080u;
-        xswap(lo[k], hi[k]);
-    });
-    // ---- forward pass 1, column pairs (2cp, 2cp+1) of the lane's half
-    f32x2 pa[4][2], pb[4][2];
-    unroll<2>([&](auto cp) {
-        f32x2 x2[8];
-        unroll<4>([&](auto k) {
-            x2[2 * k] = f32x2{px_minus128(lo[k], 2 * cp), px_minus128(lo[k], 2 * cp + 1)};
-            x2[2 * k + 1] = f32x2{px_minus128(hi[k], 2 * cp), px_minus128(hi[k], 2 * cp + 1)};
-        });
-        unroll<8>([&](auto v) {
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float c = T(v, i);
-                if constexpr (c != 0.0f) s = fma2(f32x2{c, c}, x2[i], s);
-            });
-            if constexpr (v % 2 == 0) {
-                pa[v / 2][cp] = s;
-            } else {
-                pb[v / 2][cp] = s;
-            }
-        });
-    });
-    auto swap2 = [](f32x2& x, f32x2& y) {
-        float x0 = x.x, x1 = x.y, y0 = y.x, y1 = y.y;
-        xswap(x0, y0), xswap(x1, y1);
-        x = f32x2{x0, x1}, y = f32x2{y0, y1};
-    };
-    // ---- rows 2k+h: columns (0,1) (2,3) in pa[k][0..1], (4,5) (6,7) in pb[k][0..1]
-    unroll<4>([&](auto k) { unroll<2>([&](auto cp) { swap2(pa[k][cp], pb[k][cp]); }); });
-
-    // ---- forward pass 2 (output pairs (2j, 2j+1)), quantiser, coefficient rows, D = q * Q
-    f32x2 da[4][2], db[4][2];
-    unroll<4>([&](auto k) {
-        const uint32_t row = 2u * k + h;
-        const float4* const qrow = reinterpret_cast<const float4*>(&tab[0][row * 8u]);
-        const float4* const rrow = reinterpret_cast<const float4*>(&tab[1][row * 8u]);
-        const float4 q0 = qrow[0], q1 = qrow[1], r0 = rrow[0], r1 = rrow[1];
-        const f32x2 q2[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
-        const f32x2 r2[4] = {{r0.x, r0.y}, {r0.z, r0.w}, {r1.x, r1.y}, {r1.z, r1.w}};
-        const float prow[8] = {pa[k][0].x, pa[k][0].y, pa[k][1].x, pa[k][1].y,
-                               pb[k][0].x, pb[k][0].y, pb[k][1].x, pb[k][1].y};
-        f32x2 c2[4];
-        unroll<4>([&](auto j) {
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float t0 = T(2 * j, i), t1 = T(2 * j + 1, i);
-                if constexpr (t0 != 0.0f || t1 != 0.0f) s = fma2(f32x2{t0, t1}, f32x2{prow[i], prow[i]}, s);
-            });
-            constexpr int u0 = 2 * j, u1 = 2 * j + 1;
-            constexpr int pl0 = 2 * k * 8 + u0, ph0 = (2 * k + 1) * 8 + u0;
-            constexpr int pl1 = 2 * k * 8 + u1, ph1 = (2 * k + 1) * 8 + u1;
-            constexpr bool kShort = kQMode == 2 && quantforms::jpeg_form(pl0) != quantforms::kFull &&
-                                    quantforms::jpeg_form(ph0) != quantforms::kFull &&
-                                    quantforms::jpeg_form(pl1) != quantforms::kFull &&
-                                    quantforms::jpeg_form(ph1) != quantforms::kFull;
-            f32x2 b;
-            if constexpr (kShort) {
-                auto mag = [&](auto pl, auto ph) {
-                    if constexpr (quantforms::jpeg_bias(pl) == quantforms::jpeg_bias(ph)) {
-                        return quantforms::jpeg_bias(pl);
-                    } else {
-                        return h ? quantforms::jpeg_bias(ph) : quantforms::jpeg_bias(pl);
-                    }
-                };
-                const float m0 = mag(std::integral_constant<int, pl0>{}, std::integral_constant<int, ph0>{});
-                const float m1 = mag(std::integral_constant<int, pl1>{}, std::integral_constant<int, ph1>{});
-                b = fma2(s, r2[j], f32x2{signed_mag(m0, s.x), signed_mag(m1, s.y)});
-            } else {
-                const f32x2 qa = s * r2[j];
-                const f32x2 e = fma2(-qa, q2[j], s);
-                const f32x2 d = fma2(e, r2[j], qa);
-                b = d + f32x2{signed_half(d.x), signed_half(d.y)};
-            }
-            c2[j] = f32x2{__builtin_truncf(b.x), __builtin_truncf(b.y)};
-        });
-        // coefficient row 2k+h
-        if constexpr (kRun) {
-            float4* const slot = slots + (k & 1) * 128;
-            slot[2u * lane] = make_float4(c2[0].x, c2[0].y, c2[1].x, c2[1].y);
-            slot[2u * lane + 1u] = make_float4(c2[2].x, c2[2].y, c2[3].x, c2[3].y);
-            const float4 lo4 = slot[lane], hi4 = slot[64u + lane];
-            float* const dst = coef + a.base;
-            st<kNT>(reinterpret_cast<float4*>(dst + (2u * k * a.width + 4u * lane)), lo4);
-            st<kNT>(reinterpret_cast<float4*>(dst + ((2u * k + 1u) * a.width + 4u * lane)), hi4);
-        } else {
-            const float c[8] = {c2[0].x, c2[0].y, c2[1].x, c2[1].y, c2[2].x, c2[2].y, c2[3].x, c2[3].y};
-            if (a.valid) store_row<kNT>(coef + a.base + a.off(row), c);
-        }
-        unroll<2>([&](auto cp) {
-            da[k][cp] = c2[cp] * q2[cp];
-            db[k][cp] = c2[2 + cp] * q2[2 + cp];
-        });
-    });
-    // ---- columns of D: row 2k in da[k][cp], row 2k+1 in db[k][cp]
-    unroll<4>([&](auto k) { unroll<2>([&](auto cp) { swap2(da[k][cp], db[k][cp]); }); });
-    // ---- inverse pass 1, column pairs: P[v][c] = chain_i T[i][v] D[i][c]
-    unroll<2>([&](auto cp) {
-        f32x2 d2[8];
-        unroll<4>([&](auto k) { d2[2 * k] = da[k][cp], d2[2 * k + 1] = db[k][cp]; });
-        unroll<8>([&](auto v) {
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float c = T(i, v);
-                if constexpr (c != 0.0f) s = fma2(f32x2{c, c}, d2[i], s);
-            });
-            if constexpr (v % 2 == 0) {
-                pa[v / 2][cp] = s;
-            } else {
-                pb[v / 2][cp] = s;
-            }
-        });
-    });
-    unroll<4>([&](auto k) { unroll<2>([&](auto cp) { swap2(pa[k][cp], pb[k][cp]); }); });
-    // ---- inverse pass 2 (output pairs (2j, 2j+1)), + 128, uint8, sums
-    float chain = 0.0f;
-    unroll<4>([&](auto k) {
-        const float prow[8] = {pa[k][0].x, pa[k][0].y, pa[k][1].x, pa[k][1].y,
-                               pb[k][0].x, pb[k][0].y, pb[k][1].x, pb[k][1].y};
-        float r[8];
-        unroll<4>([&](auto j) {
-            f32x2 s = {0.0f, 0.0f};
-            unroll<8>([&](auto i) {
-                constexpr float t0 = T(i, 2 * j), t1 = T(i, 2 * j + 1);
-                if constexpr (t0 != 0.0f || t1 != 0.0f) s = fma2(f32x2{t0, t1}, f32x2{prow[i], prow[i]}, s);
-            });
-            const f32x2 o = s + f32x2{128.0f, 128.0f};  // add_matrix_scalar (utils_kernels.cu:29)
-            r[2 * j] = o.x, r[2 * j + 1] = o.y;
-        });
-        const uint2 r8 = make_uint2(pack_u8x4(r[0], r[1], r[2], r[3]), pack_u8x4(r[4], r[5], r[6], r[7]));
-        if constexpr (kStats) {
-            const uint2 w = raw[k];
-            acc_xx = __builtin_amdgcn_udot4(w.x, w.x, acc_xx, false);
-            acc_xx = __builtin_amdgcn_udot4(w.y, w.y, acc_xx, false);
-            acc_xr = __builtin_amdgcn_udot4(w.x, r8.x, acc_xr, false);
-            acc_xr = __builtin_amdgcn_udot4(w.y, r8.y, acc_xr, false);
-            acc_rr = __builtin_amdgcn_udot4(r8.x, r8.x, acc_rr, false);
-            acc_rr = __builtin_amdgcn_udot4(r8.y, r8.y, acc_rr, false);
-            float e[8];
-            unroll<8>([&](auto u) { e[u] = byte_f32(u < 4 ? w.x : w.y, u & 3) - r[u]; });
-            float s = chain;
-            unroll<8>([&](auto u) { s = __builtin_fmaf(e[u], e[u], s); });
-            float to_hi = s, keep = s;
-            xswap(to_hi, keep);
-            float s2 = to_hi;
-            unroll<8>([&](auto u) { s2 = __builtin_fmaf(e[u], e[u], s2); });
-            float back = s2, to_lo = s2;
-            xswap(back, to_lo);
-            chain = to_lo;
-        }
-        if constexpr (kRecon == kRtReconU8) {
-            if (kRun || a.valid) st<kNT>(reinterpret_cast<uint2*>(recon + a.base + a.off(2u * k + h)), r8);
-        }
-    });
-    if constexpr (kStats) {
-        acc_f = (h == 0u && (kRun || a.valid)) ? chain : 0.0f;
-        if (!(kRun || a.valid)) acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
-    }
-}
-
 // Sums epilogue.  One 64-bit atomic add per field per workgroup into ONE
 // struct serialises once the workgroups are many: 8192^2 in 256-thread duo
 // workgroups (8,192 of them) took 117.5 us against 66.9 without sums, in
-// 64-thread workgroups 406 us (tools/kb_rt, profiles/r05/).  So workgroup b
-// adds into sub-slot b % kRtSpread of a spread slot (kRtSpread lines of
-// 256 B), and rt_spread_finish_kernel folds the sub-slots into the caller's
-// struct and zeroes them.  kSpread: 0 one struct, > 0 spread sub-slots,
-// -1 (A/B only) a plain store per workgroup, no atomics.
-constexpr int kRtSpread = 64;
-constexpr uint32_t kRtSpreadStride = 32;  // u64 words between sub-slots (256 B)
+// 64-thread workgroups 406 us (tools/kb_rt, profiles/r05/a/).  So each wave
+// adds its sums into sub-slot (wave % kRtSpread) of a spread slot (kRtSpread
+// lines of 256 B; rt_sse_fix and the DPP wave sums keep it free of LDS and of
+// a workgroup barrier: 78.6 us against 81.2 with __shfl_xor sums and 80.9 with
+// a workgroup reduction, profiles/r05/a/kb_rt_8192_epilogue.log), and
+// rt_spread_finish_kernel folds the sub-slots into the caller's struct and
+// zeroes them.
 
-template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSpread = kRtSpread,
-          bool kPk = false>
+// kSets: 32-tile runs per wave, the wave's runs a grid apart (the sums of all
+// of them leave in one epilogue); kSpreadN: sub-slots of the spread slot.
+template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSets = 1,
+          int kSpreadN = kRtSpread>
 __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void roundtrip_duo_kernel(
     const uint8_t* __restrict__ img, float* __restrict__ coef, uint8_t* __restrict__ recon, RtSums* __restrict__ sums,
     TileGrid g, QParams qp) {
@@ -512,11 +289,13 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
     const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, h = lane >> 5;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kW + wv);
-    const uint32_t first = wave * kRtDuoTiles;
-    float acc_f = 0.0f;
+    unsigned long long f = 0ull;  // this lane's sse_f32 chains, fixed point, over its runs
+    bool ok = true;
     uint32_t acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
 
-    if (first < g.ntiles) {
+    unroll<kSets>([&](auto it) {
+        const uint32_t first = (wave + static_cast<uint32_t>(it) * gridDim.x * kW) * kRtDuoTiles;
+        if (first >= g.ntiles) return;
         float4* const slots = stage[wv][0];
         const uint32_t by = first / g.tiles_x, bx = first - by * g.tiles_x;
         const uint32_t w32 = static_cast<uint32_t>(g.width);
@@ -527,97 +306,64 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
         }
         const DuoAddr a{static_cast<uint64_t>(by) * 8u * g.width + static_cast<uint64_t>(bx) * 8u, lane_off, w32,
                         first + t < g.ntiles};
-        if constexpr (kPk) {
-            rt_duo_body_pk<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f, acc_xx, acc_xr,
-                                                         acc_rr);
-        } else {
-            rt_duo_body<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f, acc_xx, acc_xr,
-                                                      acc_rr);
-        }
-    }
+        f32x2 acc_f2 = {0.0f, 0.0f};  // the run's tile: this lane's two chains
+        rt_duo_body<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f2, acc_xx, acc_xr,
+                                                  acc_rr);
+        if constexpr (kStats) f += rt_sse_fix(acc_f2.x, ok) + rt_sse_fix(acc_f2.y, ok);
+    });
 
-    if constexpr (kStats && kSpread == -2) {  // A/B: the sums computed, no reduction (kept alive)
-        if ((acc_xx ^ acc_rr ^ acc_xr ^ __float_as_uint(acc_f)) == 0x9e3779b9u)
-            reinterpret_cast<unsigned long long*>(sums)[threadIdx.x] = 1ull;
-    } else if constexpr (kStats && (kSpread == -3 || kSpread == -4)) {
-        // per-wave: wave sums, lane 0 adds into sub-slot (wave % kRtSpread); no LDS, no barrier
-        const float fx = __builtin_rintf(acc_f * kRtFixScale);
-        const bool f_ok = fx < 0x1p40f;  // false for NaN
-        unsigned long long f = f_ok ? static_cast<unsigned long long>(fx) : 0ull;
-        unsigned long long e8, xx;
-        if constexpr (kSpread == -4) {
-            f = wave_sum_dpp(f);
-            e8 = wave_sum_dpp(acc_xx + acc_rr - 2u * acc_xr), xx = wave_sum_dpp(acc_xx);
-        } else {
-            f = wave_sum_u64(f);
-            e8 = wave_sum_u64(acc_xx + acc_rr - 2u * acc_xr), xx = wave_sum_u64(acc_xx);
-        }
-        const bool bad = __builtin_amdgcn_ballot_w64(!f_ok) != 0;
+    if constexpr (kStats) {
+        // the wave's sums: sse_f32 in fixed point (64-bit), and sse_u8 / sum_x2
+        // packed in one 64-bit word (each below 2^30 over a wave: 32 pixels
+        // per lane and run, <= 255^2 each, kSets <= 8); DPP reductions, then
+        // lane 0 adds into sub-slot (wave % kSpreadN) of the spread slot: no
+        // LDS, no barrier
+        static_assert(kSets <= 8, "packed integer sums");
+        const uint32_t e8 = acc_xx + acc_rr - 2u * acc_xr;
+        unsigned long long ints = (static_cast<unsigned long long>(acc_xx) << 32) | e8;
+        f = wave_sum_dpp(f), ints = wave_sum_dpp(ints);
+        const bool bad = __builtin_amdgcn_ballot_w64(!ok) != 0;
         if (lane == 0u) {
-            auto* const dst = reinterpret_cast<unsigned long long*>(sums) + (wave % kRtSpread) * kRtSpreadStride;
+            auto* const dst = reinterpret_cast<unsigned long long*>(sums) + (wave % kSpreadN) * kRtSpreadStride;
             if (f) atomicAdd(dst, f);
             if (bad) atomicOr(dst, kRtSseF32Invalid);
-            if (e8) atomicAdd(dst + 1, e8);
-            if (xx) atomicAdd(dst + 2, xx);
-        }
-    } else if constexpr (kStats) {
-        const float fx = __builtin_rintf(acc_f * kRtFixScale);
-        const bool f_ok = fx < 0x1p40f;  // false for NaN
-        unsigned long long f = f_ok ? static_cast<unsigned long long>(fx) : 0ull;
-        unsigned long long e8 = static_cast<unsigned long long>(acc_xx + acc_rr - 2u * acc_xr);
-        unsigned long long xx = static_cast<unsigned long long>(acc_xx);
-        f = wave_sum_u64(f), e8 = wave_sum_u64(e8), xx = wave_sum_u64(xx);
-        if (__builtin_amdgcn_ballot_w64(!f_ok) != 0) f |= kRtSseF32Invalid;
-        __shared__ unsigned long long part[kW][3];
-        if (lane == 0u) part[wv][0] = f, part[wv][1] = e8, part[wv][2] = xx;
-        __syncthreads();
-        if (threadIdx.x < 3u) {
-            unsigned long long s = 0, bad = 0;
-            for (uint32_t k = 0; k < kW; ++k) {
-                s += part[k][threadIdx.x] & ~kRtSseF32Invalid;
-                bad |= part[k][threadIdx.x] & kRtSseF32Invalid;
-            }
-            auto* const words = reinterpret_cast<unsigned long long*>(sums);
-            if constexpr (kSpread < 0) {
-                words[blockIdx.x * 4u + threadIdx.x] = s | bad;
-            } else {
-                auto* const dst = words + (kSpread > 0 ? (blockIdx.x % kSpread) * kRtSpreadStride : 0u) + threadIdx.x;
-                if (s) atomicAdd(dst, s);
-                if (bad) atomicOr(dst, kRtSseF32Invalid);
-            }
+            if (ints & 0xffffffffull) atomicAdd(dst + 1, ints & 0xffffffffull);
+            if (ints >> 32) atomicAdd(dst + 2, ints >> 32);
         }
     }
 }
 
-// Folds the kRtSpread sub-slots of a spread slot into *dst (overwriting it,
-// or adding to it when accumulate) and zeroes them: one wave, lane i reads
-// sub-slot i.
-__global__ __launch_bounds__(64) void rt_spread_finish_kernel(RtSums* __restrict__ dst,
-                                                              unsigned long long* __restrict__ slot, int accumulate) {
-    static_assert(kRtSpread <= 64, "one wave folds the sub-slots");
-    const uint32_t l = threadIdx.x;
-    unsigned long long v[3] = {0ull, 0ull, 0ull};
-    if (l < static_cast<uint32_t>(kRtSpread)) {
-        unroll<3>([&](auto f) {
-            v[f] = slot[l * kRtSpreadStride + f];
-            slot[l * kRtSpreadStride + f] = 0ull;
-        });
-    }
-    unroll<3>([&](auto f) {
-        const unsigned long long sum = wave_sum_u64(v[f] & ~kRtSseF32Invalid);
-        const bool bad = __builtin_amdgcn_ballot_w64((v[f] & kRtSseF32Invalid) != 0ull) != 0ull;
-        if (l == 0u) {
-            auto* const d = reinterpret_cast<unsigned long long*>(dst) + f;
-            unsigned long long out = accumulate ? *d + sum : sum;
-            if (bad) out |= kRtSseF32Invalid;
-            *d = out;
-        }
-    });
-}
-
-inline dim3 roundtrip_duo_grid(const TileGrid& g, uint32_t block = 256) {
-    const uint32_t waves = (g.ntiles + kRtDuoTiles - 1u) / kRtDuoTiles, per = block / 64u;
+inline dim3 roundtrip_duo_grid(const TileGrid& g, uint32_t block = 256, uint32_t sets = 1) {
+    const uint32_t runs = (g.ntiles + kRtDuoTiles - 1u) / kRtDuoTiles, per = block / 64u;
+    const uint32_t waves = (runs + sets - 1u) / sets;
     return dim3((waves + per - 1u) / per);
 }
+
+namespace rt_duo_detail {
+// 256-thread workgroups, 6 waves per SIMD (74 VGPRs, no spills; 7 and 8
+// spill and run slower, tools/kb_rt, profiles/r05/a/).  Whole runs only
+// (tiles_x a multiple of 32, launch_roundtrip checks): the kRun = false kernel
+// (ragged widths, 92 VGPRs) is slower than the tile kernel there (4096 x 4104:
+// 36.9 against 31.9 us with sums, profiles/r05/b/kb_rt_ragged.log).
+constexpr int kDuoRtBlock = 256, kDuoRtWaves = 6;
+template <bool kStats, int kQMode, int kRecon>
+hipError_t go(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread, const TileGrid& g,
+              const QParams& qp, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, kQMode, kRecon, true, kDuoRtBlock, kDuoRtWaves>),
+                       roundtrip_duo_grid(g, kDuoRtBlock), dim3(kDuoRtBlock), 0, s, img, coef, recon,
+                       reinterpret_cast<RtSums*>(spread), g, qp);
+    return hipGetLastError();
+}
+template <int kRecon>
+hipError_t go_r(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread, const TileGrid& g,
+                const QParams& qp, int qmode, hipStream_t s) {
+    if (spread) {
+        return qmode == 2 ? go<true, 2, kRecon>(img, coef, recon, spread, g, qp, s)
+                          : go<true, 1, kRecon>(img, coef, recon, spread, g, qp, s);
+    }
+    return qmode == 2 ? go<false, 2, kRecon>(img, coef, recon, nullptr, g, qp, s)
+                      : go<false, 1, kRecon>(img, coef, recon, nullptr, g, qp, s);
+}
+}  // namespace rt_duo_detail
 
 }  // namespace hpdct

@@ -139,26 +139,30 @@ hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t 
  *            truncate) or HPDCT_F32 (no clamp), or NULL for none (as
  *            hpdct_inverse F32 -> recon_type on d_coef)
  *   d_sums   device struct, or NULL: the quality sums below (overwritten).  The
- *            kernel adds into a 24-byte library slot kept per d_sums pointer
- *            (allocated zeroed on first use, 1024 at a time) and a one-wave
- *            kernel then moves it over *d_sums: ~1.8 us per launch less than
- *            a memset of *d_sums before the kernel.  The memset is the
- *            fallback when a slot would need an allocation inside a stream
- *            capture, or past 65536 pointers.  Two launches in flight at once
- *            with the same d_sums on different streams race, as they would on
- *            the struct itself.
+ *            kernel adds into a 16 KiB library "spread slot" kept per d_sums
+ *            pointer (64 sub-slots on separate 256-B lines, so the atomics of
+ *            many waves do not queue on one line; allocated zeroed on first
+ *            use, 256 at a time) and a one-wave kernel then folds it into
+ *            *d_sums and zeroes it: no memset before the kernel.  Without a
+ *            slot (an allocation would be needed inside a stream capture, or
+ *            past 16384 pointers) the launch memsets *d_sums and takes the
+ *            tile-per-lane kernel.  Two launches in flight at once with the
+ *            same d_sums on different streams race, as they would on the
+ *            struct itself.
  * Built-in T, the library Q, level shift 128; coefficients and reconstruction
  * are bit-identical to the two separate calls.  HBM traffic per pixel: 1 B
  * read, 4 B (+1 or 4 B) written, against 10 B for the two calls.
  * PEEN = 100 sqrt(sse / sum_x2) %, MSE = sse / (height*width) (the
  * definitions of the README table). */
 typedef struct hpdct_roundtrip_sums {
-    uint64_t sse_f32_fx; /* sum (x - (R+128))^2 in units of 2^-16 (HPDCT_SSE_F32_UNIT): each tile's
-                            fp32 partial sum (an fma chain over its 64 pixels, so NOT the exact sum:
-                            relative error ~1e-9 on a 8192^2 frame) rounded to the unit, the tiles
-                            then added exactly in any order.  Bit 63 (HPDCT_SSE_F32_INVALID) is set,
-                            sticky, when some tile's partial sum is non-finite or >= 2^24 (an
-                            extreme caller table on the IEEE path): the field then holds no sum */
+    uint64_t sse_f32_fx; /* sum (x - (R+128))^2 in units of 2^-16 (HPDCT_SSE_F32_UNIT): per tile four
+                            fp32 partial sums, one per (row parity, column parity) class of its
+                            pixels (an fma chain over the class's 16 pixels in row-major order, so
+                            NOT the exact sum: relative error ~1e-10 on a 8192^2 frame), each
+                            rounded to the unit, then all added exactly in any order.  Bit 63
+                            (HPDCT_SSE_F32_INVALID) is set, sticky, when some partial sum is
+                            non-finite or >= 2^24 (an extreme caller table on the IEEE path): the
+                            field then holds no sum */
     uint64_t sse_u8;     /* sum (x - u8(R+128))^2, exact */
     uint64_t sum_x2;     /* sum x^2, exact */
 } hpdct_roundtrip_sums;
@@ -168,10 +172,10 @@ hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_r
                                 hpdct_roundtrip_sums* d_sums, int64_t height, int64_t width, void* stream);
 
 /* The same round trip, but the frame's quality sums are ADDED to *d_sums,
- * which the caller has zeroed (d_sums required): one launch, no second kernel
- * (~1 us per launch less than hpdct_roundtrip_u8).  A pipeline that owns a ring
- * of per-frame sums slots zeroes the ring once, with one memset for many
- * frames, and gets the same per-frame sums (or a batch total, if frames share a
+ * which the caller has zeroed (d_sums required; the same spread slot and fold
+ * kernel, which adds instead of overwriting).  A pipeline that owns a ring of
+ * per-frame sums slots zeroes the ring once, with one memset for many frames,
+ * and gets the same per-frame sums (or a batch total, if frames share a
  * slot). */
 hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef, void* d_recon,
                                            hpdct_dtype recon_type, hpdct_roundtrip_sums* d_sums, int64_t height,

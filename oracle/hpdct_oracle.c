@@ -314,6 +314,38 @@ void oracle_idct(const float* coef, int64_t h, int64_t w, const float* T, const 
         }
 }
 
+/* The round trip's device sum sse_f32_fx (hpdct_roundtrip_u8, include/hpdct.h;
+ * the build's own definition -- the reference computes PEEN/MSE on the host):
+ * per 8x8 tile, four fp32 chains s = fmaf(e, e, s) from +0, one per (row
+ * parity, column parity) class of the tile's pixels in row-major order, with
+ * e = x - r (x the uint8 pixel as float, r the fp32 reconstruction R + 128);
+ * each chain rounded to a multiple of 2^-16 (rintf(s * 65536)) and added as
+ * uint64.  Returns the sum, with bit 63 set when some chain is non-finite or
+ * its fixed point is >= 2^40 (that chain then adds nothing).                */
+uint64_t oracle_rt_sse_f32_fx(const uint8_t* x, const float* r, int64_t h, int64_t w) {
+    uint64_t sum = 0, bad = 0;
+    for (int64_t by = 0; by < h / 8; ++by)
+        for (int64_t bx = 0; bx < w / 8; ++bx) {
+            float c[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+            for (int v = 0; v < 8; ++v)
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t i = (by * 8 + v) * w + bx * 8 + u;
+                    const float e = (float)x[i] - r[i];
+                    c[v & 1][u & 1] = fmaf(e, e, c[v & 1][u & 1]);
+                }
+            for (int p = 0; p < 2; ++p)
+                for (int q = 0; q < 2; ++q) {
+                    const float fx = rintf(c[p][q] * 65536.0f);
+                    if (fx < 0x1p40f) {
+                        sum += (uint64_t)fx;
+                    } else {
+                        bad = 1;
+                    }
+                }
+        }
+    return bad ? (sum | (1ull << 63)) : sum;
+}
+
 /* PEEN / MSE (README.md:62-69 names them; no code in the reference):
  * PEEN = 100 * sqrt(sum (x - y)^2 / sum x^2), MSE = mean (x - y)^2.       */
 void oracle_quality(const float* x, const float* y, int64_t n, double* peen, double* mse) {

@@ -47,6 +47,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_fill_rand_u8.argtypes = [vp, i64, ctypes.c_uint32]
         L.oracle_fill_hash_u8.argtypes = [vp, i64, ctypes.c_uint64, i64]
         L.oracle_quality.argtypes = [vp, vp, i64, vp, vp]
+        L.oracle_rt_sse_f32_fx.argtypes = [vp, vp, i64, i64]
+        L.oracle_rt_sse_f32_fx.restype = ctypes.c_uint64
         L.oracle_u8_to_f32.argtypes = [vp, vp, i64]
         L.oracle_f32_to_u8.argtypes = [vp, vp, i64]
         L.oracle_default_quant.argtypes = [vp]
@@ -163,6 +165,14 @@ def to_u8(a: np.ndarray) -> np.ndarray:
     o = np.empty(a.shape, np.uint8)
     lib().oracle_f32_to_u8(_p(a), _p(o), a.size)
     return o
+
+
+def rt_sse_f32_fx(img: np.ndarray, r: np.ndarray) -> int:
+    """The round trip's sse_f32_fx (hpdct_oracle.c oracle_rt_sse_f32_fx): img
+    uint8 (h x w), r the fp32 reconstruction R + 128 of the same shape."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    r = np.ascontiguousarray(r, dtype=np.float32)
+    return int(lib().oracle_rt_sse_f32_fx(_p(img), _p(r), img.shape[0], img.shape[1]))
 
 
 def quality(x: np.ndarray, y: np.ndarray):

@@ -353,3 +353,38 @@ def test_c3_8192_roundtrip_one_pass(hp, oracle, dev, golden):
     assert abs(q["mse_u8"] - g["mse_u8"]) < 1e-9 * g["mse_u8"]
     assert abs(q["peen_u8_pct"] - g["peen_u8"]) < 1e-9 * g["peen_u8"]
     assert got["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
+
+
+@pytest.mark.parametrize("mapping", ["auto", "tile"])
+@pytest.mark.parametrize("h,w", [(8, 256), (64, 512), (1000, 1008), (256, 2048), (2048, 4096)])
+def test_sse_f32_is_the_four_chain_definition(hp, oracle, dev, mapping, h, w):
+    """sse_f32_fx bit for bit against the oracle's restatement of its
+    definition (oracle_rt_sse_f32_fx: four fp32 chains per tile, one per
+    (row parity, column parity) class, each rounded to 2^-16): the
+    two-lanes-per-tile kernel (AUTO, widths a multiple of 256) and the tile
+    kernel (forced, or ragged widths, or the fp32 reconstruction) give the
+    same value; accumulate mode adds it."""
+    import torch
+    img = np.random.default_rng(h * 7 + w).integers(0, 256, (h, w), dtype=np.uint8)
+    q = oracle.fdct(img)
+    r = oracle.idct(q)
+    want = oracle.rt_sse_f32_fx(img, r)
+    assert want < (1 << 53)
+    x = to_dev(img, dev)
+    hp.set_mapping(mapping)
+    try:
+        _, _, s8 = hp.roundtrip(x, recon_dtype=torch.uint8, sums=True)
+        _, _, s0 = hp.roundtrip(x, sums=True)
+        _, _, sf = hp.roundtrip(x, recon_dtype=torch.float32, sums=True)
+        buf = torch.zeros(3, dtype=torch.int64, device=dev)
+        coef = torch.empty((h, w), dtype=torch.float32, device=dev)
+        call = hp.bind_roundtrip(x, coef, None, buf, accumulate=True)
+        call()
+        call()
+        acc = hp.sums_from_buffer(buf)
+    finally:
+        hp.set_mapping("auto")
+    for got in (s8, s0, sf):
+        assert got["sse_f32"] * 65536 == want
+    assert acc["sse_f32"] * 65536 == 2 * want
+    assert acc["sse_u8"] == 2 * s8["sse_u8"] and acc["sum_x2"] == 2 * s8["sum_x2"]

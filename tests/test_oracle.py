@@ -221,3 +221,21 @@ def test_fdct_threads_equals_fdct(oracle, h, w, threads):
     a = oracle.fdct_threads(img, threads)
     b = oracle.fdct(img)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_rt_sse_f32_definition_known_answers():
+    """oracle_rt_sse_f32_fx (the round trip's sse_f32 definition, checked bit
+    for bit against the GPU in tests/test_gpu_roundtrip.py): known answers."""
+    import oracle
+    img = np.full((16, 24), 100, dtype=np.uint8)
+    assert oracle.rt_sse_f32_fx(img, img.astype(np.float32)) == 0
+    # e = -1 everywhere: each of the 4 chains of a tile holds 16, a tile 64
+    assert oracle.rt_sse_f32_fx(img, img.astype(np.float32) + 1.0) == 6 * 64 * 65536
+    # e = 0.5 at one pixel only
+    r = img.astype(np.float32)
+    r[3, 5] -= 0.5
+    assert oracle.rt_sse_f32_fx(img, r) == 65536 // 4
+    # a non-finite chain sets bit 63 and adds nothing
+    r[0, 0] = np.inf
+    v = oracle.rt_sse_f32_fx(img, r)
+    assert v >> 63 == 1 and (v & ((1 << 63) - 1)) == 65536 // 4

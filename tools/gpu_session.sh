@@ -18,6 +18,7 @@
 #                         kb:8192:64:3:occsz:16 -> log kb3_occsz_8192.log
 #   pmcsq:<args>          SQ/GRBM counter pass over kbench3 <args>
 #   pmctcc:<args>         TCC/TA counter pass over kbench3 <args>
+#   pmcrd:<args>          TCC read and write request pass over kbench3 <args>
 #   verify_quant:<xmax>   tests/tools/verify_quant1 (exhaustive quantiser proof)
 #   kbd[:<args>]          tools/kb_decode (int8 -> fp32 decode A/B)
 #   devinfo               HIP device attributes the launch code reads
@@ -35,6 +36,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 TCC="TCC_EA0_WRREQ TCC_EA0_WRREQ_DRAM_CREDIT_STALL TA_DATA_STALLED_BY_TC_CYCLES TA_ADDR_STALLED_BY_TC_CYCLES GRBM_GUI_ACTIVE"
+RD="TCC_EA0_RDREQ TCC_EA0_WRREQ GRBM_GUI_ACTIVE"
 
 step() {  # step <name> <timeout-s> <cmd...>
     local name=$1 t=$2; shift 2
@@ -80,6 +82,7 @@ for s in "$@"; do
     kb) step "kb3_${p[4]}_${p[1]}" 300 tools/kbench3 "${p[@]:1}" || exit $? ;;
     pmcsq) pmc "sq_${p[4]}_${p[1]}" "$SQ" "${p[@]:1}" || exit $? ;;
     pmctcc) pmc "tcc_${p[4]}_${p[1]}" "$TCC" "${p[@]:1}" || exit $? ;;
+    pmcrd) pmc "rd_${p[4]}_${p[1]}" "$RD" "${p[@]:1}" || exit $? ;;
     verify_quant) step "verify_quant1_${p[1]:-4096}" 300 tests/tools/verify_quant1 "${p[1]:-4096}" || exit $? ;;
     devinfo) step devinfo 120 python3 tools/devinfo.py || exit $? ;;
     kbd) step kb_decode 300 tools/kb_decode "${p[@]:1}" || exit $? ;;

@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "hpdct_rt_duo.hpp"
+#include "kbench_rtduo_pk.hpp"
 
 using namespace hpdct;
 
@@ -42,23 +42,69 @@ void tile_rt(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipS
     hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, 2, 2, false, 256>), roundtrip_grid(c.g, 256), dim3(256),
                        0, s, img, coef, static_cast<void*>(recon), kStats ? c.sums : nullptr, c.g, c.qp);
 }
-template <bool kStats, int kQ, int kB, int kW, bool kRun = true>
-void duo_rt(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
-    if (kStats) (void)hipMemsetAsync(c.sums, 0, sizeof(RtSums), s);
-    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, kQ, kRtReconU8, kRun, kB, kW, 0>), roundtrip_duo_grid(c.g, kB),
-                       dim3(kB), 0, s, img, coef, recon, kStats ? c.sums : nullptr, c.g, c.qp);
+// the product: the kernel adds into a zeroed spread slot, the finish kernel
+// folds it over the caller's struct (no memset)
+unsigned long long* g_spread = nullptr;
+template <bool kStats, int kB, int kW, bool kPk = false, bool kRun = true>
+void duo_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    RtSums* const sp = reinterpret_cast<RtSums*>(kStats ? g_spread : nullptr);
+    if constexpr (kPk) {
+        hipLaunchKernelGGL((roundtrip_duo_pk_kernel<kStats, 2, kRtReconU8, kB, kW>), roundtrip_duo_grid(c.g, kB),
+                           dim3(kB), 0, s, img, coef, recon, sp, c.g, c.qp);
+    } else {
+        hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, 2, kRtReconU8, kRun, kB, kW>), roundtrip_duo_grid(c.g, kB),
+                           dim3(kB), 0, s, img, coef, recon, sp, c.g, c.qp);
+    }
+    if (kStats) hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+}
+// finish-kernel A/B: kMode 0 the product's (shfl sums), 1 no finish at all
+// (timing only: the slot keeps growing), 2 DPP sums instead of shfl
+__global__ __launch_bounds__(64) void finish_dpp(RtSums* __restrict__ dst, unsigned long long* __restrict__ slot,
+                                                 int accumulate) {
+    const uint32_t l = threadIdx.x;
+    unsigned long long v[3] = {0ull, 0ull, 0ull};
+    if (l < static_cast<uint32_t>(kRtSpread)) {
+        unroll<3>([&](auto f) {
+            v[f] = slot[l * kRtSpreadStride + f];
+            slot[l * kRtSpreadStride + f] = 0ull;
+        });
+    }
+    unroll<3>([&](auto f) {
+        const unsigned long long sum = wave_sum_dpp(v[f] & ~kRtSseF32Invalid);
+        const bool bad = __builtin_amdgcn_ballot_w64((v[f] & kRtSseF32Invalid) != 0ull) != 0ull;
+        if (l == 0u) {
+            auto* const d = reinterpret_cast<unsigned long long*>(dst) + f;
+            unsigned long long out = accumulate ? *d + sum : sum;
+            if (bad) out |= kRtSseF32Invalid;
+            *d = out;
+        }
+    });
+}
+template <int kMode>
+void duo_fin(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6>), roundtrip_duo_grid(c.g, 256),
+                       dim3(256), 0, s, img, coef, recon,
+                       reinterpret_cast<RtSums*>(kMode == 1 ? g_spread + (1u << 18) : g_spread), c.g, c.qp);
+    if (kMode == 0) hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+    if (kMode == 2) hipLaunchKernelGGL(finish_dpp, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
 }
 
-// the product candidate: the kernel adds into a zeroed spread slot, the
-// finish kernel folds it over the caller's struct (no memset)
-unsigned long long* g_spread = nullptr;
-template <bool kStats, int kB, int kW, int kSpread, bool kPk = false>
-void duo_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
-    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, 2, kRtReconU8, true, kB, kW, kSpread, kPk>), roundtrip_duo_grid(c.g, kB),
-                       dim3(kB), 0, s, img, coef, recon,
-                       reinterpret_cast<RtSums*>(kSpread == -1 || kSpread == -2 ? g_spread + (1u << 18) : g_spread),
+// runs per wave and sub-slots A/B
+template <int kSets, int kN>
+void duo_sn(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6, kSets, kN>),
+                       roundtrip_duo_grid(c.g, 256, kSets), dim3(256), 0, s, img, coef, recon,
+                       reinterpret_cast<RtSums*>(g_spread), c.g, c.qp);
+    hipLaunchKernelGGL(rt_spread_finish_kernel<kN>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+}
+
+// the tile kernel with the product's sums path (spread sub-slot 0 + finish)
+template <bool kStats>
+void tile_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_kernel<kRtReconU8, kStats, 2, 2, false, 256>), roundtrip_grid(c.g, 256), dim3(256), 0,
+                       s, img, coef, static_cast<void*>(recon), reinterpret_cast<RtSums*>(kStats ? g_spread : nullptr),
                        c.g, c.qp);
-    if (kSpread > 0 || kSpread == -3 || kSpread == -4) hipLaunchKernelGGL(rt_spread_finish_kernel, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+    if (kStats) hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
 }
 
 struct V {
@@ -98,36 +144,32 @@ int main(int argc, char** argv) {
     CK(hipMemset(g_spread, 0, 1u << 22));
 
     std::vector<V> vars = {
-        {"rtduo", "tile rt + sums (product)", tile_rt<true>, true},
-        {"rtduo", "duo + sums, w6, spread 64 + finish", duo_sp<true, 256, 6, 64>, true},
-        {"rtduo", "duo + sums, w6, per-wave atomics", duo_sp<true, 256, 6, -3>, true},
-        {"rtduo", "duo + sums, w6, per-wave atomics, DPP sums", duo_sp<true, 256, 6, -4>, true},
-        {"rtduo", "duo + sums, w6, sums not reduced", duo_sp<true, 256, 6, -2>, false},
-        {"rtduo", "duo pk + sums, w6, per-wave atomics, DPP", duo_sp<true, 256, 6, -4, true>, true},
-        {"rtduo", "duo + sums, w6, per-wave DPP, 64-thr WGs", duo_sp<true, 64, 6, -4>, true},
-        {"rtduo", "duo + sums, w6, per-wave DPP, 512-thr WGs", duo_sp<true, 512, 6, -4>, true},
-        {"rtduo", "tile rt no sums", tile_rt<false>, false},
-        {"rtduo", "duo rt no sums, w6", duo_rt<false, 2, 256, 6>, false},
-        {"rtduo", "duo no sums, w6, 64-thr WGs", duo_sp<false, 64, 6, 0>, false},
-        {"rtduo", "tile rt + sums (product) again", tile_rt<true>, true},
-        {"rtduo", "duo + sums, w6, per-wave atomics, DPP again", duo_sp<true, 256, 6, -4>, true},
+        {"rtduo", "tile rt + sums, spread + finish", tile_sp<true>, true},
+        {"rtduo", "duo + sums (product: 1 run/wave, 64 sub-slots)", duo_sp<true, 256, 6>, true},
+        {"rtduo", "duo + sums, 256 sub-slots", duo_sn<1, 256>, true},
+        {"rtduo", "duo + sums, 2 runs/wave", duo_sn<2, 64>, true},
+        {"rtduo", "duo + sums, 2 runs/wave, 256 sub-slots", duo_sn<2, 256>, true},
+        {"rtduo", "duo + sums, 4 runs/wave, 256 sub-slots", duo_sn<4, 256>, true},
+        {"rtduo", "duo + sums, no finish kernel (timing)", duo_fin<1>, false},
+        {"rtduo", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"rtduo", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"rtduo", "duo + sums, 2 runs/wave, 256 sub-slots again", duo_sn<2, 256>, true},
+        {"rtduo", "duo + sums, 256 sub-slots again", duo_sn<1, 256>, true},
+        {"rtduo", "tile rt + sums, spread + finish again", tile_sp<true>, true},
         // any width (tiles_x not a multiple of 32): the ragged kernel only
-        {"ragged", "tile rt + sums (product)", tile_rt<true>, true},
-        {"ragged", "duo rt + sums, ragged kernel w5", duo_rt<true, 2, 256, 5, false>, true},
-        {"ragged", "duo rt no sums, ragged kernel w5", duo_rt<false, 2, 256, 5, false>, false},
-        {"ragged", "duo rt + sums, ragged kernel, 6-op quotient", duo_rt<true, 1, 256, 5, false>, true},
+        {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
+        {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
+        {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
+        {"ragged", "duo + sums, ragged kernel, w6", duo_sp<true, 256, 6, false, false>, true},
     };
     vars.erase(std::remove_if(vars.begin(), vars.end(),
                               [&](const V& v) { return only == "all" ? v.group == "ragged" : v.group != only; }),
                vars.end());
-    printf("frame %llux%llu, %d sets, VGPRs: tile %d, duo w5 %d w6 %d w7 %d w8 %d, ragged w5 %d\n",
-           (unsigned long long)H, (unsigned long long)W, nsets,
-           vgprs_of(roundtrip_kernel<kRtReconU8, true, 2, 2, false, 256>),
-           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 5, 0>),
-           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6, 0>),
-           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 7, 0>),
-           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 8, 0>),
-           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, false, 256, 5, 0>));
+    printf("frame %llux%llu, %d sets, VGPRs: tile %d, duo %d, duo pk %d, ragged %d\n", (unsigned long long)H,
+           (unsigned long long)W, nsets, vgprs_of(roundtrip_kernel<kRtReconU8, true, 2, 2, false, 256>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6>),
+           vgprs_of(roundtrip_duo_pk_kernel<true, 2, kRtReconU8, 256, 6>),
+           vgprs_of(roundtrip_duo_kernel<true, 2, kRtReconU8, false, 256, 5>));
 
     std::vector<uint8_t*> img(nsets), rec(nsets);
     std::vector<float*> coef(nsets);

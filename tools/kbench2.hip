@@ -194,8 +194,10 @@ void rt_two_kernels(const void* in, void* out, const Ctx& c, hipStream_t s) {
 }
 template <int kRecon, bool kStats, bool kFast>
 void rt_fused(const void* in, void* out, const Ctx& c, hipStream_t s) {
-    (void)launch_roundtrip_impl(static_cast<const uint8_t*>(in), g_coef2[set_of(in)], kRecon == kRtReconNone ? nullptr : out,
-                     kRecon, kStats ? g_sums : nullptr, c.g, c.qp, kFast, s, true);
+    if (kStats) (void)hipMemsetAsync(g_sums, 0, sizeof(RtSums), s);
+    (void)rt_detail::go_r<kRecon>(static_cast<const uint8_t*>(in), g_coef2[set_of(in)],
+                                  kRecon == kRtReconNone ? nullptr : out, kStats ? g_sums : nullptr, c.g, c.qp,
+                                  kFast, s);
 }
 
 template <int kRaw, bool kMemset = true>

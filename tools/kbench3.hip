@@ -166,12 +166,12 @@ void issue_go(const void*, void* out, const Ctx& c, hipStream_t s) {
 // (set = j * W + wave: at step j all waves work on consecutive sets, so the
 // chip-wide write front is W x 16 KiB) with the next set's rows prefetched
 // into registers; W = kWavesPerCU x CUs.
-template <bool kPrefetch>
-__global__ __launch_bounds__(256) void pat_band(const uint8_t* __restrict__ in, float* __restrict__ out, TileGrid g,
-                                                uint32_t nsets) {
+template <bool kPrefetch, uint32_t kWpb = 4>
+__global__ __launch_bounds__(64 * kWpb) void pat_band(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                      TileGrid g, uint32_t nsets) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = gridDim.x * 4u;
-    uint32_t s = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWpb;
+    uint32_t s = __builtin_amdgcn_readfirstlane(blockIdx.x * kWpb + (threadIdx.x >> 6));
     auto base_of = [&](uint32_t set) {
         const uint32_t t0 = set * 64u, ty = t0 / g.tiles_x, tx = t0 - ty * g.tiles_x;
         return static_cast<uint64_t>(ty) * 8u * g.width + static_cast<uint64_t>(tx) * 8u;
@@ -212,6 +212,11 @@ void pat_grid_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        static_cast<float*>(out), c.g, nsets);
 }
 
+// the headline's access pattern in one-wave workgroups (the product's dispatch
+// shape since round 3), at most kWaves resident per CU (0: uncapped)
+template <uint32_t kWaves>
+void pat_grid_cap1_go(const void* in, void* out, const Ctx& c, hipStream_t s);
+
 // ---- occupancy caps through dynamic LDS (round 3, session 3): kWg workgroups
 // per CU at most, so a 256-thread workgroup gives 4 x kWg waves per CU.  The
 // kernels do not use the dynamic part; it only reserves LDS.
@@ -236,6 +241,13 @@ void pat_grid_cap_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
     const uint32_t nsets = c.g.ntiles / 64u;
     static const size_t dyn = cap_for(pat_band<false>, kWg);
     hipLaunchKernelGGL((pat_band<false>), dim3(nsets / 4u), dim3(256), dyn, s, static_cast<const uint8_t*>(in),
+                       static_cast<float*>(out), c.g, nsets);
+}
+template <uint32_t kWaves>
+void pat_grid_cap1_go(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    const uint32_t nsets = c.g.ntiles / 64u;
+    static const size_t dyn = kWaves ? cap_for(pat_band<false, 1>, kWaves) : 0;
+    hipLaunchKernelGGL((pat_band<false, 1>), dim3(nsets), dim3(64), dyn, s, static_cast<const uint8_t*>(in),
                        static_cast<float*>(out), c.g, nsets);
 }
 // the tools-only tile kernel (scalar or packed) with kWg workgroups per CU at most
@@ -437,6 +449,14 @@ int main(int argc, char** argv) {
         {"specpat", "pat one set per wave (grid) again", pat_grid_go, 5, 4, false},
         // occupancy caps (dynamic LDS): does the one-set-per-wave dispatch gain DRAM efficiency with fewer
         // waves per CU, as the banded schedule did (0.77 at 4 w/cu), and can the packed math keep up there?
+        // round 5: the headline's limiter at cap 7, counters in their own passes
+        {"lim", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"lim", "pat 1-wave WGs, cap 4 w/cu", pat_grid_cap1_go<4>, 5, 4, false},
+        {"lim", "pat 1-wave WGs, cap 7 w/cu", pat_grid_cap1_go<7>, 5, 4, false},
+        {"lim", "pat 1-wave WGs, uncapped", pat_grid_cap1_go<0>, 5, 4, false},
+        {"lim1", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"lim4", "pat 1-wave WGs, cap 4 w/cu", pat_grid_cap1_go<4>, 5, 4, false},
+        {"lim7", "pat 1-wave WGs, cap 7 w/cu", pat_grid_cap1_go<7>, 5, 4, false},
         {"occpat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
         {"occpat", "pat grid cap 4 w/cu", pat_grid_cap_go<1>, 5, 4, false},
         {"occpat", "pat grid cap 8 w/cu", pat_grid_cap_go<2>, 5, 4, false},
