@@ -156,6 +156,11 @@ int main(int argc, char** argv) {
         {"rtduo", "duo + sums, 2 runs/wave, 256 sub-slots again", duo_sn<2, 256>, true},
         {"rtduo", "duo + sums, 256 sub-slots again", duo_sn<1, 256>, true},
         {"rtduo", "tile rt + sums, spread + finish again", tile_sp<true>, true},
+        // counter passes (rocprofv3 --pmc): one variant each
+        {"pmc_tile", "tile rt + sums, spread + finish", tile_sp<true>, true},
+        {"pmc_duo", "duo + sums (product)", duo_sp<true, 256, 6>, true},
+        {"pmc_duo_nosums", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"pmc_tile_nosums", "tile rt no sums", tile_rt<false>, false},
         // any width (tiles_x not a multiple of 32): the ragged kernel only
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
