@@ -161,6 +161,14 @@ int main(int argc, char** argv) {
         {"pmc_duo", "duo + sums (product)", duo_sp<true, 256, 6>, true},
         {"pmc_duo_nosums", "duo no sums", duo_sp<false, 256, 6>, false},
         {"pmc_tile_nosums", "tile rt no sums", tile_rt<false>, false},
+        {"pmc_pk", "duo pk + sums", duo_sp<true, 256, 6, true>, true},
+        {"pmc_pk_nosums", "duo pk no sums", duo_sp<false, 256, 6, true>, false},
+        {"pk", "duo + sums (product)", duo_sp<true, 256, 6>, true},
+        {"pk", "duo pk + sums", duo_sp<true, 256, 6, true>, true},
+        {"pk", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"pk", "duo pk no sums", duo_sp<false, 256, 6, true>, false},
+        {"pk", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"pk", "duo pk + sums again", duo_sp<true, 256, 6, true>, true},
         // any width (tiles_x not a multiple of 32): the ragged kernel only
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},

@@ -27,12 +27,14 @@ pass() {  # pass <name> <counters> <program> <args...>
     return $rc
 }
 
-for g in pmc_tile pmc_duo pmc_duo_nosums pmc_tile_nosums; do
+RT_GROUPS=${RT_GROUPS:-pmc_tile pmc_duo pmc_duo_nosums pmc_tile_nosums}
+LIM_GROUPS=${LIM_GROUPS-lim1 lim4 lim7}
+for g in $RT_GROUPS; do
     for set in SQ TCC RD; do
         pass "${g}_${set}" "${!set}" "$ROOT/tools/kb_rt" 8192 16 1 "$g" || exit $?
     done
 done
-for g in lim1 lim4 lim7; do
+for g in $LIM_GROUPS; do
     for set in SQ TCC RD; do
         pass "${g}_${set}" "${!set}" "$ROOT/tools/kbench3" 8192 16 1 "$g" 16 || exit $?
     done
