@@ -12,9 +12,9 @@ SAN    := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit
 CXXF   := -std=c++17 -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I$(ROOT)/include -I$(PKG)/csrc -I$(PKG)/build $(SAN)
 CF     := -std=c11 -ffp-contract=off -fno-fast-math $(SAN)
 HOST   := hpdct_api hpdct_compat hpdct_stream
-KOBJ   := $(wildcard $(PKG)/build/hpdct_frames.o $(PKG)/build/hpdct_fwd_u8.o $(PKG)/build/hpdct_fwd_f32.o $(PKG)/build/hpdct_inv.o \
-            $(PKG)/build/hpdct_inv_i8.o $(PKG)/build/hpdct_roundtrip.o $(PKG)/build/hpdct_baselines.o \
-            $(PKG)/build/hpdct_decode.o)
+# the kernel objects, as the library's Makefile lists them (its KOBJ line)
+PKG_KOBJ := $(filter build/%.o,$(shell sed -n 's/^KOBJ *:= *//p' $(PKG)/Makefile))
+KOBJ   := $(wildcard $(PKG_KOBJ:%=$(PKG)/%))
 
 all: $(OUT)/asan_host_check
 

@@ -608,6 +608,8 @@ int main(int argc, char** argv) {
         {"i8cap", "fwd u8->i8 jpegq b256 cap 24 w/cu", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | kVarJpegQ, 6>, 2, 1, true},
         {"i8cap", "fwd u8->i8 jpegq b256 (product) again", prod_i8_fwd<I8 | kVarJpegQ>, 2, 1, true},
         {"i8cap", "fwd u8->i8 jpegq b64 cap 20 w/cu again", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 20>, 2, 1, true},
+        // the u8 -> int8 product alone, for counter passes (tools/gpu_session.sh pmcsq:...:i8lim)
+        {"i8lim", "fwd u8->i8 jpegq b64 cap 20 w/cu (product)", prod_i8_fwd_cap<(I8 & ~(3u << 12)) | (1u << 12) | kVarJpegQ, 20>, 2, 1, true},
         // round trip workgroup size
         {"jqrtb", "rt + sums, jpegq b512", rt_q<true, 2>, 6, 1, true},
         {"jqrtb", "rt + sums, jpegq b256", rt_qb<true, 2, 256>, 6, 1, true},
