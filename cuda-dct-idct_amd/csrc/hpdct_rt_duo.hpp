@@ -44,9 +44,10 @@
 // (broadcast reads), and a short JPEG form (hpdct_quant_forms.h) is used at a
 // column when BOTH positions have one, the verified 6-op quotient otherwise.
 //
-// sse_f32 is the tile kernel's per-tile fp32 chain over the 64 pixels in row
-// order: row 2k in lanes 0..31, its sum moved to lanes 32..63 for row 2k+1,
-// and back for row 2k+2 (two swaps per row pair).
+// sse_f32 is the tile kernel's: four fp32 chains per tile, one per (row
+// parity, column parity) class in row-major order (hpdct_roundtrip.hpp).  A
+// lane owns rows of one parity (2k + h), so it keeps two of them, even and odd
+// columns in the halves of one packed register: no cross-lane hand-off.
 #pragma once
 
 #include "hpdct_octet.hpp"
@@ -93,6 +94,21 @@ struct DuoAddr {
     bool valid;         // this lane's tile exists
     __device__ __forceinline__ uint32_t off(uint32_t r) const { return lane_off + r * width; }
 };
+
+// sse_f32 of one chain in fixed point (rt_sse_fix), added to the lane's
+// 32-bit halves split at 2^22: fx = hi * 2^22 + lo exactly (fx is an integer
+// below 2^40, hi = floor(fx / 2^22) < 2^18, lo = fx - hi * 2^22 < 2^22 by
+// one exact fma).  Over a wave (64 lanes, 2 chains, <= 8 runs) both sums
+// stay below 2^32.
+__device__ __forceinline__ void rt_sse_split(float chain, bool& ok, uint32_t& hi, uint32_t& lo) {
+    const float fx = __builtin_rintf(chain * kRtFixScale);
+    const bool good = fx < 0x1p40f;  // false for NaN
+    ok = ok && good;
+    const float h = __builtin_floorf(fx * 0x1p-22f);
+    const float l = __builtin_fmaf(-h, 0x1p22f, fx);
+    hi += good ? static_cast<uint32_t>(h) : 0u;
+    lo += good ? static_cast<uint32_t>(l) : 0u;
+}
 
 }  // namespace
 
@@ -206,9 +222,12 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
             slot[2u * lane + 1u] = make_float4(c[4], c[5], c[6], c[7]);
             const float4 lo4 = slot[lane], hi4 = slot[64u + lane];
             // [0, 1 KiB): row 2k of the 32 tiles; [1 KiB, 2 KiB): row 2k+1
-            float* const dst = coef + a.base;
-            st<kNT>(reinterpret_cast<float4*>(dst + (2u * k * a.width + 4u * lane)), lo4);
-            st<kNT>(reinterpret_cast<float4*>(dst + ((2u * k + 1u) * a.width + 4u * lane)), hi4);
+            // byte offsets in 32 bits (< 32 * width bytes from the wave's
+            // base), so both stores take the SGPR-base + VGPR-offset form
+            char* const dst = reinterpret_cast<char*>(coef + a.base);
+            const uint32_t o_lo = (2u * k * a.width + 4u * lane) * 4u, o_hi = o_lo + a.width * 4u;
+            st<kNT>(reinterpret_cast<float4*>(dst + o_lo), lo4);
+            st<kNT>(reinterpret_cast<float4*>(dst + o_hi), hi4);
         } else {
             if (a.valid) store_row<kNT>(coef + a.base + a.off(row), c);
         }
@@ -263,14 +282,19 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
 // workgroups (8,192 of them) took 117.5 us against 66.9 without sums, in
 // 64-thread workgroups 406 us (tools/kb_rt, profiles/r05/a/).  So each wave
 // adds its sums into sub-slot (wave % kRtSpread) of a spread slot (kRtSpread
-// lines of 256 B; rt_sse_fix and the DPP wave sums keep it free of LDS and of
-// a workgroup barrier: 78.6 us against 81.2 with __shfl_xor sums and 80.9 with
-// a workgroup reduction, profiles/r05/a/kb_rt_8192_epilogue.log), and
+// lines of 256 B; DPP wave sums keep it free of LDS and of a workgroup
+// barrier: 78.6 us against 81.2 with __shfl_xor sums and 80.9 with a
+// workgroup reduction, profiles/r05/a/kb_rt_8192_epilogue.log), and
 // rt_spread_finish_kernel folds the sub-slots into the caller's struct and
-// zeroes them.
+// zeroes them.  Four 32-bit DPP sums instead of two 64-bit ones (sse_f32
+// split at 2^22, rt_sse_split): 1,096 VALU per wave instead of 1,163 and
+// 73.7-74.0 us against 74.5-75.2 (profiles/r05/f/).
 
 // kSets: 32-tile runs per wave, the wave's runs a grid apart (the sums of all
 // of them leave in one epilogue); kSpreadN: sub-slots of the spread slot.
+// Two more kSpreadN values exist for tools/kb_rt's decomposition of the sums'
+// cost only: 0 writes one plain 32-B record per wave (no atomics), < 0
+// computes the sums and skips the atomics when sums is null.
 template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSets = 1,
           int kSpreadN = kRtSpread>
 __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void roundtrip_duo_kernel(
@@ -289,7 +313,7 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
     const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, h = lane >> 5;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kW + wv);
-    unsigned long long f = 0ull;  // this lane's sse_f32 chains, fixed point, over its runs
+    uint32_t f_hi = 0u, f_lo = 0u;  // this lane's sse_f32 chains in fixed point over its runs, split at 2^22
     bool ok = true;
     uint32_t acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
 
@@ -307,28 +331,40 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
         const DuoAddr a{static_cast<uint64_t>(by) * 8u * g.width + static_cast<uint64_t>(bx) * 8u, lane_off, w32,
                         first + t < g.ntiles};
         f32x2 acc_f2 = {0.0f, 0.0f};  // the run's tile: this lane's two chains
-        rt_duo_body<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f2, acc_xx, acc_xr,
-                                                  acc_rr);
-        if constexpr (kStats) f += rt_sse_fix(acc_f2.x, ok) + rt_sse_fix(acc_f2.y, ok);
+        rt_duo_body<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f2, acc_xx, acc_xr, acc_rr);
+        if constexpr (kStats) {
+            rt_sse_split(acc_f2.x, ok, f_hi, f_lo);
+            rt_sse_split(acc_f2.y, ok, f_hi, f_lo);
+        }
     });
 
     if constexpr (kStats) {
-        // the wave's sums: sse_f32 in fixed point (64-bit), and sse_u8 / sum_x2
-        // packed in one 64-bit word (each below 2^30 over a wave: 32 pixels
-        // per lane and run, <= 255^2 each, kSets <= 8); DPP reductions, then
-        // lane 0 adds into sub-slot (wave % kSpreadN) of the spread slot: no
-        // LDS, no barrier
-        static_assert(kSets <= 8, "packed integer sums");
+        // the wave's sums: four 32-bit DPP sums (each add takes its DPP
+        // operand directly; every one stays below 2^32 over a wave: 32 pixels
+        // per lane and run, kSets <= 8), sse_f32 rebuilt as 64 bits in scalar
+        // registers; lane 0 adds into sub-slot (wave % kSpreadN) of the
+        // spread slot: no LDS, no barrier.  Its atomics take a per-lane zero
+        // offset, so they stay single atomics (no uniform-address rewrite).
+        static_assert(kSets <= 8, "32-bit wave sums");
         const uint32_t e8 = acc_xx + acc_rr - 2u * acc_xr;
-        unsigned long long ints = (static_cast<unsigned long long>(acc_xx) << 32) | e8;
-        f = wave_sum_dpp(f), ints = wave_sum_dpp(ints);
+        const uint32_t sh = wave_sum_dpp(f_hi), sl = wave_sum_dpp(f_lo);
+        const uint32_t sx = wave_sum_dpp(acc_xx), se = wave_sum_dpp(e8);
+        const unsigned long long fs = (static_cast<unsigned long long>(sh) << 22) + sl;
         const bool bad = __builtin_amdgcn_ballot_w64(!ok) != 0;
-        if (lane == 0u) {
-            auto* const dst = reinterpret_cast<unsigned long long*>(sums) + (wave % kSpreadN) * kRtSpreadStride;
-            if (f) atomicAdd(dst, f);
-            if (bad) atomicOr(dst, kRtSseF32Invalid);
-            if (ints & 0xffffffffull) atomicAdd(dst + 1, ints & 0xffffffffull);
-            if (ints >> 32) atomicAdd(dst + 2, ints >> 32);
+        if (lane == 0u && (kSpreadN > 0 || sums)) {
+            uint32_t z = 0u;
+            asm volatile("" : "+v"(z));
+            if constexpr (kSpreadN == 0) {
+                auto* const dst = reinterpret_cast<unsigned long long*>(sums) + wave * 4u + z;
+                dst[0] = bad ? (fs | kRtSseF32Invalid) : fs, dst[1] = se, dst[2] = sx;
+            } else {
+                constexpr uint32_t kN = kSpreadN < 0 ? -kSpreadN : kSpreadN;
+                auto* const dst = reinterpret_cast<unsigned long long*>(sums) + (wave % kN) * kRtSpreadStride + z;
+                if (fs) atomicAdd(dst, fs);
+                if (bad) atomicOr(dst, kRtSseF32Invalid);
+                if (se) atomicAdd(dst + 1, static_cast<unsigned long long>(se));
+                if (sx) atomicAdd(dst + 2, static_cast<unsigned long long>(sx));
+            }
         }
     }
 }

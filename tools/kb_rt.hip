@@ -98,6 +98,20 @@ void duo_sn(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipSt
     hipLaunchKernelGGL(rt_spread_finish_kernel<kN>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
 }
 
+// sums decomposition: kMode 0 sums computed, no atomics (null sums); 1 one
+// plain 32-B record per wave (no contention); timing only
+template <int kMode>
+void duo_dec(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    if (kMode == 0) {
+        hipLaunchKernelGGL((roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6, 1, -64>), roundtrip_duo_grid(c.g, 256),
+                           dim3(256), 0, s, img, coef, recon, nullptr, c.g, c.qp);
+    } else {
+        hipLaunchKernelGGL((roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6, 1, 0>), roundtrip_duo_grid(c.g, 256),
+                           dim3(256), 0, s, img, coef, recon, reinterpret_cast<RtSums*>(g_spread + (1u << 18)), c.g,
+                           c.qp);
+    }
+}
+
 // the tile kernel with the product's sums path (spread sub-slot 0 + finish)
 template <bool kStats>
 void tile_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
@@ -170,6 +184,20 @@ int main(int argc, char** argv) {
         {"pk", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
         {"pk", "duo pk + sums again", duo_sp<true, 256, 6, true>, true},
         // any width (tiles_x not a multiple of 32): the ragged kernel only
+        {"ab", "duo + sums (product)", duo_sp<true, 256, 6>, true},
+        {"ab", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"ab", "tile rt + sums, spread + finish", tile_sp<true>, true},
+        {"ab", "duo + sums, no atomics (timing)", duo_dec<0>, false},
+        {"ab", "duo + sums, plain record per wave (timing)", duo_dec<1>, false},
+        {"ab", "duo + sums, no finish kernel (timing)", duo_fin<1>, false},
+        {"ab", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"ab", "duo no sums again", duo_sp<false, 256, 6>, false},
+        {"occ", "duo + sums (product)", duo_sp<true, 256, 6>, true},
+        {"occ", "duo + sums, w7", duo_sp<true, 256, 7>, true},
+        {"occ", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"occ", "duo no sums, w7", duo_sp<false, 256, 7>, false},
+        {"occ", "duo no sums, w8", duo_sp<false, 256, 8>, false},
+        {"occ", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
@@ -276,3 +304,4 @@ int main(int argc, char** argv) {
     }
     return 0;
 }
+

@@ -74,6 +74,47 @@ OP_KERNEL(k_cvt_pk_i16_i32, "v_cvt_pk_i16_i32 %0, %0, %1")
 OP_KERNEL(k_ashr_pk_i8, "v_ashr_pk_i8_i32 %0, %0, %1, 0")
 OP_KERNEL(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca")
 
+// 64-bit operands (register pairs): packed fp32 and the 64-bit address add
+#define OP64_KERNEL(NAME, ASM)                                                                \
+    __global__ __launch_bounds__(256) void NAME(uint32_t* out, int iters, uint32_t seed) {    \
+        uint64_t b = (uint64_t)(seed ^ threadIdx.x) * 0x100000001ull, c = 0x3f0000003f000000ull; \
+        uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,        \
+                 a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                       \
+        for (int i = 0; i < iters; ++i) {                                                     \
+            asm volatile(ASM : "+v"(a0) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a1) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a2) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a3) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a4) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a5) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a6) : "v"(b), "v"(c));                                    \
+            asm volatile(ASM : "+v"(a7) : "v"(b), "v"(c));                                    \
+        }                                                                                     \
+        const uint64_t x = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                             \
+        out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)x ^ (uint32_t)(x >> 32);              \
+    }
+OP64_KERNEL(k_pk_fma_f32, "v_pk_fma_f32 %0, %1, %2, %0")
+OP64_KERNEL(k_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
+OP64_KERNEL(k_pk_mul_f32, "v_pk_mul_f32 %0, %0, %1")
+OP64_KERNEL(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
+
+// v_permlane32_swap_b32: both operands in and out, 4 pairs x 2 per iteration
+__global__ __launch_bounds__(256) void k_permlane32_swap(uint32_t* out, int iters, uint32_t seed) {
+    uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+             a7 = a0 + 7;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a0), "+v"(a1));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a2), "+v"(a3));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a4), "+v"(a5));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a6), "+v"(a7));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a1), "+v"(a2));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a3), "+v"(a4));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a5), "+v"(a6));
+        asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a7), "+v"(a0));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 struct K {
     const char* name;
     void (*fn)(uint32_t*, int, uint32_t);
@@ -90,6 +131,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&out, (size_t)blocks * 256 * 4));
     const K ks[] = {{"v_fmac_f32", k_fmac},
                     {"v_fma_f32 (VOP3)", k_fma3},
+                    {"v_pk_fma_f32", k_pk_fma_f32},
+                    {"v_pk_add_f32", k_pk_add_f32},
+                    {"v_pk_mul_f32", k_pk_mul_f32},
+                    {"v_lshl_add_u64", k_lshl_add_u64},
+                    {"v_permlane32_swap_b32", k_permlane32_swap},
                     {"v_add_f32", k_add},
                     {"v_mul_f32", k_mul},
                     {"v_subrev_f32", k_subrev},
