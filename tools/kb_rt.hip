@@ -192,6 +192,9 @@ int main(int argc, char** argv) {
         {"ab", "duo + sums, no finish kernel (timing)", duo_fin<1>, false},
         {"ab", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
         {"ab", "duo no sums again", duo_sp<false, 256, 6>, false},
+        {"lx", "duo + sums (product)", duo_sp<true, 256, 6>, true},
+        {"lx", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"lx", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
         {"occ", "duo + sums (product)", duo_sp<true, 256, 6>, true},
         {"occ", "duo + sums, w7", duo_sp<true, 256, 7>, true},
         {"occ", "duo no sums", duo_sp<false, 256, 6>, false},
@@ -271,7 +274,7 @@ int main(int argc, char** argv) {
                                    c0[i], c1[i], r0[i], r1[i]);
                             ++n;
                         }
-                    return 1;
+                    if (!getenv("KB_CONTINUE")) return 1;
                 }
             }
         }
@@ -304,4 +307,5 @@ int main(int argc, char** argv) {
     }
     return 0;
 }
+
 

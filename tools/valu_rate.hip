@@ -73,6 +73,11 @@ OP_KERNEL(k_pk_add, "v_pk_add_u16 %0, %0, %1")
 OP_KERNEL(k_cvt_pk_i16_i32, "v_cvt_pk_i16_i32 %0, %0, %1")
 OP_KERNEL(k_ashr_pk_i8, "v_ashr_pk_i8_i32 %0, %0, %1, 0")
 OP_KERNEL(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca")
+OP_KERNEL(k_mov, "v_mov_b32 %0, %1")
+OP_KERNEL(k_mov_dpp_ror8, "v_mov_b32_dpp %0, %1 row_ror:8 row_mask:0xf bank_mask:0x3")
+OP_KERNEL(k_mov_dpp_ror8_self, "v_mov_b32_dpp %0, %0 row_ror:8 row_mask:0xf bank_mask:0xc")
+OP_KERNEL(k_add_u32_dpp, "v_add_u32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+OP_KERNEL(k_fmac_dpp, "v_fmac_f32_dpp %0, %1, %2 row_ror:8 row_mask:0xf bank_mask:0xf")
 
 // 64-bit operands (register pairs): packed fp32 and the 64-bit address add
 #define OP64_KERNEL(NAME, ASM)                                                                \
@@ -136,6 +141,11 @@ int main(int argc, char** argv) {
                     {"v_pk_mul_f32", k_pk_mul_f32},
                     {"v_lshl_add_u64", k_lshl_add_u64},
                     {"v_permlane32_swap_b32", k_permlane32_swap},
+                    {"v_mov_b32", k_mov},
+                    {"v_mov_b32_dpp row_ror:8 bank_mask:0x3", k_mov_dpp_ror8},
+                    {"v_mov_b32_dpp self row_ror:8 bank_mask:0xc", k_mov_dpp_ror8_self},
+                    {"v_add_u32_dpp row_shr:1", k_add_u32_dpp},
+                    {"v_fmac_f32_dpp row_ror:8", k_fmac_dpp},
                     {"v_add_f32", k_add},
                     {"v_mul_f32", k_mul},
                     {"v_subrev_f32", k_subrev},
