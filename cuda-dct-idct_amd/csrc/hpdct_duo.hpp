@@ -106,6 +106,15 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
                                                                 float shift) {
     const TSource<kBuiltinT, false> T(t_dev);
     const uint32_t lane = threadIdx.x & 63u, t = lane >> 1, h = lane & 1u;
+    // Q and RN(1/Q) per lane from LDS (lane h quantises rows 4h..4h+3).  Taken
+    // from the kernel arguments with a select on h, both rows' values sat in
+    // SGPRs beside a caller's T (64 more): past the SGPR budget, so the
+    // compiler spilled them to VGPR lanes (208 v_readlane/v_writelane per wave).
+    __shared__ __attribute__((aligned(16))) float tab[2][64];
+    if constexpr (kQuant) {
+        if (threadIdx.x < 64u) tab[0][threadIdx.x] = qp.q.v[threadIdx.x], tab[1][threadIdx.x] = qp.r.v[threadIdx.x];
+        __syncthreads();
+    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t first = wave * kDuoTiles;
     if (first >= g.ntiles) return;
@@ -143,18 +152,17 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
             unroll<8>([&](auto i) { s = T.template mac<u * 8 + i>(row[i], s); });
             dst[u] = s;
         });
-        if constexpr (kQuant && (kVar & kVarFastDivChecked) != 0) {  // row 4h+k of Q and 1/Q
-            float qv[8], rv[8];
-            unroll<8>([&](auto u) {
-                qv[u] = h ? qp.q.v[(4 + k) * 8 + u] : qp.q.v[k * 8 + u];
-                rv[u] = h ? qp.r.v[(4 + k) * 8 + u] : qp.r.v[k * 8 + u];
-            });
-            quantise_row_checked(dst, qv, rv);
-        } else if constexpr (kQuant) {  // row 4h+k of Q: two kernel-argument values, one select
-            unroll<8>([&](auto u) {
-                const float qv = h ? qp.q.v[(4 + k) * 8 + u] : qp.q.v[k * 8 + u];
-                dst[u] = quantise<kVar>(dst[u], qv, 0.0f);
-            });
+        if constexpr (kQuant) {  // row 4h+k of Q and 1/Q
+            const uint32_t r = 4u * h + k;
+            const float4 q0 = ld4(&tab[0][r * 8u]), q1 = ld4(&tab[0][r * 8u + 4u]);
+            const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            if constexpr ((kVar & kVarFastDivChecked) != 0) {
+                const float4 r0 = ld4(&tab[1][r * 8u]), r1 = ld4(&tab[1][r * 8u + 4u]);
+                const float rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+                quantise_row_checked(dst, qv, rv);
+            } else {
+                unroll<8>([&](auto u) { dst[u] = quantise<kVar>(dst[u], qv[u], 0.0f); });
+            }
         }
     }, o);
     duo_store<kVar>(out, g, run, run_base, p.base, p.valid, slot_all, t, h, o);
