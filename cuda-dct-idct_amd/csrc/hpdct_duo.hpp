@@ -258,6 +258,14 @@ __global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float*
     constexpr uint32_t S = kDuoStride<kVar>;
     const TSource<kBuiltinT, false> T(t_dev);
     const uint32_t lane = threadIdx.x & 63u, t = lane >> 1, h = lane & 1u;
+    // Q per lane from LDS, as in fdct_duo_kernel (selects between kernel
+    // arguments beside a caller's T overran the SGPR budget: 128-260
+    // v_readlane/v_writelane per wave)
+    __shared__ __attribute__((aligned(16))) float tab[64];
+    if constexpr (kQ) {
+        if (threadIdx.x < 64u) tab[threadIdx.x] = q.v[threadIdx.x];
+        __syncthreads();
+    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock<kVar> / 64u) + threadIdx.x / 64u);
     const uint32_t first = wave * kDuoTiles;
     if (first >= g.ntiles) return;
@@ -284,11 +292,11 @@ __global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float*
         unroll<8>([&](auto k) {
             const float4 v = ld4(src + run_base + k * g.width + 4u * lane);
             const float vv[4] = {v.x, v.y, v.z, v.w};
+            float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (kInv && kQ) q4 = ld4(&tab[k * 8 + 4u * hh]);  // Q[k][4hh..4hh+3]
+            const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
             float e[4];
-            unroll<4>([&](auto c) {
-                const float qv = kInv && kQ ? (hh ? q.v[k * 8 + 4 + c] : q.v[k * 8 + c]) : 0.0f;
-                e[c] = prep(vv[c], qv);
-            });
+            unroll<4>([&](auto c) { e[c] = prep(vv[c], qq[c]); });
             if constexpr (kWb)
                 st<kNT>(reinterpret_cast<float4*>(wb + run_base + k * g.width) + lane, make_float4(e[0], e[1], e[2], e[3]));
             lds4(slot_all + (lane >> 1) * S + k * 8u + 4u * hh, e[0], e[1], e[2], e[3]);
@@ -307,10 +315,10 @@ __global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float*
                 b = ld4(src + p.base + (4u * h + k) * g.width + 4u);
             }
             const float raw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-            unroll<8>([&](auto j) {
-                const float qv = kInv && kQ ? (h ? q.v[(4 + k) * 8 + j] : q.v[k * 8 + j]) : 0.0f;
-                x[k][j] = prep(raw[j], qv);
-            });
+            float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+            if constexpr (kInv && kQ) q0 = ld4(&tab[(4u * h + k) * 8u]), q1 = ld4(&tab[(4u * h + k) * 8u + 4u]);
+            const float qq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            unroll<8>([&](auto j) { x[k][j] = prep(raw[j], qq[j]); });
             if constexpr (kWb) {
                 if (p.valid) {
                     float4* dst = reinterpret_cast<float4*>(wb + p.base + (4u * h + k) * g.width);
@@ -341,6 +349,13 @@ __global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float*
     });
     // column chains: C[v][u] = sum_i T[v][i] R[i][u] (forward) / sum_i T[i][v] R[i][u] (inverse)
     float o[4][8];  // o[c][v] = output (v, 4h+c)
+    float qcol[8][4];  // forward: Q[v][4h + c]
+    if constexpr (!kInv && kQ) {
+        unroll<8>([&](auto v) {
+            const float4 q4 = ld4(&tab[v * 8 + 4u * h]);
+            qcol[v][0] = q4.x, qcol[v][1] = q4.y, qcol[v][2] = q4.z, qcol[v][3] = q4.w;
+        });
+    }
     unroll<4>([&](auto c) {
         unroll<8>([&](auto v) {
             float s = 0.0f;
@@ -348,8 +363,7 @@ __global__ __launch_bounds__(kBlock<kVar>) void rowfirst_duo_kernel(const float*
             if constexpr (kInv) {
                 s = s + shift;  // add_matrix_scalar, no clamp
             } else if constexpr (kQ) {
-                const float qv = h ? q.v[v * 8 + 4 + c] : q.v[v * 8 + c];
-                s = quantise<kVar>(s, qv, 0.0f);
+                s = quantise<kVar>(s, qcol[v][c], 0.0f);
             }
             o[c][v] = s;
         });
