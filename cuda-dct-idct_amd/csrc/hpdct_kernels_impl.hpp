@@ -399,20 +399,23 @@ __device__ __forceinline__ void store_row_lds(float4* __restrict__ slot, float* 
 
 // The same for a set that straddles a tile-row boundary (ragged widths): its
 // first k tiles end tile row ty (row segment at seg), the other 64-k start
-// tile row ty+1 (at seg2).  Each store instruction then writes two contiguous
-// runs instead of falling back to one 32-B store per lane.
+// tile row ty+1, 7 * width + 8k elements further on.  Each store instruction
+// then writes two contiguous runs instead of falling back to one 32-B store
+// per lane.  float4 q holds half q%2 of tile q/2's row: tiles >= k lie
+// 7 * width + 8k - 4 * 2k = 7 * width elements past the run they would
+// continue, so every address is seg + 16 q bytes, plus jump = 28 * width
+// bytes from q = 2k on: one SGPR base and a 32-bit lane offset per store
+// (the offsets do not depend on the row, so they are computed once per set).
 template <bool kNT>
-__device__ __forceinline__ void store_row_lds2(float4* __restrict__ slot, float* __restrict__ seg,
-                                               float* __restrict__ seg2, uint32_t k, uint32_t lane,
-                                               const float (&c)[8]) {
+__device__ __forceinline__ void store_row_lds2(float4* __restrict__ slot, float* __restrict__ seg, uint32_t jump,
+                                               uint32_t k, uint32_t lane, const float (&c)[8]) {
     slot[2 * lane] = make_float4(c[0], c[1], c[2], c[3]);
     slot[2 * lane + 1] = make_float4(c[4], c[5], c[6], c[7]);
     const float4 a = slot[lane];
     const float4 b = slot[64 + lane];
-    // float4 q holds half q%2 of tile q/2's row: tiles < k go to seg, the rest to seg2
     const uint32_t q0 = lane, q1 = 64u + lane, h = 2u * k;
-    st<kNT>(reinterpret_cast<float4*>(q0 < h ? seg + 4u * q0 : seg2 + 4u * (q0 - h)), a);
-    st<kNT>(reinterpret_cast<float4*>(q1 < h ? seg + 4u * q1 : seg2 + 4u * (q1 - h)), b);
+    st_at<kNT>(seg, 16u * q0 + (q0 < h ? 0u : jump), a);
+    st_at<kNT>(seg, 16u * q1 + (q1 < h ? 0u : jump), b);
 }
 
 // Per-wave walk over 64-tile sets: one set per wave, wave w = set w.
@@ -478,10 +481,9 @@ struct RowSink {
                 return;
             }
             if ((kVar & kVarStraddle) != 0 && split != 0u) {
-                // next tile row's first tile: seg - (width - 8k) + 8 width (dense pitch: tiles_x = width / 8)
-                const uint64_t seg2 = seg + 7u * width + 8u * split;
-                store_row_lds2<kNT>(slots + (v & 1) * 128, plane + seg + v * width, plane + seg2 + v * width, split,
-                                    threadIdx.x & 63u, c);
+                // the next tile row's first tile: 7 * width + 8 split elements past seg (dense pitch)
+                store_row_lds2<kNT>(slots + (v & 1) * 128, plane + seg + v * width,
+                                    28u * static_cast<uint32_t>(width), split, threadIdx.x & 63u, c);
                 return;
             }
         }
