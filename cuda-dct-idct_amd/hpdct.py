@@ -421,7 +421,7 @@ def bind_roundtrip(image, coef, recon=None, sums_buf=None, *, stream=None, heigh
     """Pre-resolved round-trip launch (like bind): a zero-argument callable.
     sums_buf: an int64 CUDA tensor of 3 elements, or None.  accumulate=True:
     the frame's sums are added to sums_buf, which the caller zeroes
-    (hpdct_roundtrip_u8_accumulate: one kernel, no sums finish kernel)."""
+    (hpdct_roundtrip_u8_accumulate: the same kernels, the finish adds)."""
     if accumulate and sums_buf is None:
         raise HpdctError(1, "accumulate=True needs a sums buffer")
     args = _roundtrip_args(image, coef, recon, sums_buf, height, width, stream)
