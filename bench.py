@@ -83,6 +83,10 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank flow with several ranks on one GPU)")
+    ap.add_argument("--extras-timeout-s", type=float, default=420.0,
+                    help="watchdog on the extras (the other kernels, C4's RCCL gather, C5): if they have not "
+                         "finished by then, rank 0 prints the headline line with extras marked as timed out "
+                         "and every rank exits; 0 disables it")
     return ap.parse_args()
 
 
@@ -330,11 +334,30 @@ def main():
     # ------------------------------------------------------------ other kernels of the path
     if not args.no_extras:
         extras = {}
+        # A hang in the extras (a first multi-GPU run of the RCCL gather, say)
+        # must not cost the headline line: the watchdog prints it and exits.
+        watchdog = None
+        if args.extras_timeout_s > 0:
+            import threading
+
+            def _extras_timed_out():
+                if rank == 0:
+                    line = dict(result)
+                    line["extras"] = {"error": f"extras did not finish within {args.extras_timeout_s:.0f} s "
+                                               "(watchdog); headline measured before them"}
+                    print(json.dumps(line), file=json_out, flush=True)
+                os._exit(0)
+
+            watchdog = threading.Timer(args.extras_timeout_s, _extras_timed_out)
+            watchdog.daemon = True
+            watchdog.start()
         try:
             _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop, imgs,
                     outs, px, n, extras)
         except Exception as e:  # report, keep the headline line
             extras["error"] = f"{type(e).__name__}: {e}"[:500]
+        if watchdog is not None:
+            watchdog.cancel()
         result["extras"] = extras
         c4 = extras.get("c4", {})
         # the north_star row-shard figures (C4, 16384^2 over the ranks), top level
