@@ -506,9 +506,24 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         qd = hpdct.quality_from_sums(hpdct.sums_from_buffer(sums_buf), px)
         one_ms = rms1 / steps
         sums_one = hpdct.sums_from_buffer(sums_buf)
+        # the same with the fp32 reconstruction (R + 128 unclamped, the
+        # reference's float output): coefficients + fp32 pixels + sums, 9 B/px.
+        # Checked: set 0's fp32 pixels equal the two-kernel inverse's, and its
+        # sums equal the uint8-reconstruction pass's (the same definition)
+        r_ref = r.clone()
+        sums_f = torch.zeros(3, dtype=torch.int64, device=dev)
+        onef = [hpdct.bind_roundtrip(imgs[s], outs[s], rec[s % 2], sums_f, stream=stream)
+                for s in range(args.sets)]
+        rmsf, kf, _ = timed_loop(onef, steps, 4)
+        onef[0]()
+        torch.cuda.synchronize()
+        f32_recon_exact = bool(torch.equal(rec[0], r_ref))
+        f32_sums_equal = hpdct.sums_from_buffer(sums_f) == sums_one
+        f32_ms = rmsf / steps
+        del onef, sums_f, r_ref
         # the same with a caller-zeroed ring of per-frame sums slots
-        # (hpdct_roundtrip_u8_accumulate: one kernel per launch, no sums
-        # finish kernel).  The warm-up accumulates into a ring of its own; the
+        # (hpdct_roundtrip_u8_accumulate: the frame's sums are added to its
+        # slot by the same finish kernel).  The warm-up accumulates into a ring of its own; the
         # timed launches go to a fresh zeroed ring, one slot each, so after the
         # region every slot must hold exactly its frame's sums (ring_sums_exact)
         ref_sums = []
@@ -556,6 +571,10 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums in one "
                                   "pass (the round trip + a one-wave kernel that moves the sums from the library's "
                                   "slot over the caller's struct); bit-identical to the two kernels"),
+            "one_pass_f32_recon": dict(_line(px, f32_ms, float(kf.mean()), 9, world),
+                                       recon_equals_two_kernels=f32_recon_exact, sums_equal_u8_pass=f32_sums_equal,
+                                       note="hpdct_roundtrip_u8 with HPDCT_F32: coefficients + fp32 R+128 (the "
+                                            "reference's float output) + PEEN/MSE sums in one pass"),
             "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
                                        ring_sums_exact=ring_exact,
                                        note="hpdct_roundtrip_u8_accumulate, one slot per timed launch of a fresh "

@@ -78,8 +78,10 @@ hipError_t launch_rt_tile_f32(const uint8_t* img, float* coef, void* recon, RtSu
                               const QParams& qp, int fast, hipStream_t s);
 hipError_t launch_rt_tile_none(const uint8_t* img, float* coef, void* recon, RtSums* sums, const TileGrid& g,
                                const QParams& qp, int fast, hipStream_t s);
-hipError_t launch_rt_duo(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread,
+hipError_t launch_rt_duo(const uint8_t* img, float* coef, void* recon, int recon_kind, unsigned long long* spread,
                          const TileGrid& g, const QParams& qp, int fast, hipStream_t s);
+hipError_t launch_rt_duo_f32(const uint8_t* img, float* coef, void* recon, unsigned long long* spread,
+                             const TileGrid& g, const QParams& qp, int fast, hipStream_t s);
 hipError_t launch_rt_finish(RtSums* dst, unsigned long long* spread, bool accumulate, hipStream_t s);
 
 // A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch

@@ -92,25 +92,23 @@ hipError_t tile(const uint8_t* img, float* coef, void* recon, int recon_kind, Rt
 }  // namespace
 
 // The kernel: the two-lanes-per-tile round trip (hpdct_rt_duo.hpp) for the
-// verified quotient (fast 1 or 2) with a uint8 reconstruction or none, when
-// its sums (if any) have a spread slot, the width is a multiple of 256
-// pixels (whole 32-tile runs per wave) and the mapping is not forced to
-// "tile"; 8192^2 with sums 76.3-76.7 us against 79.7 for the tile kernel with
-// the same sums path and 82.4 with round 4's memset, without sums 67.0
-// against 76.8 (tools/kb_rt, profiles/r05/b/).  Otherwise the tile-per-lane
-// kernel (fp32 reconstruction, IEEE division, ragged widths, forced tile
-// mapping), with its sums in the spread slot's sub-slot 0 when it has one.
+// verified quotient (fast 1 or 2) with any reconstruction, when its sums (if
+// any) have a spread slot, the width is a multiple of 256 pixels (whole
+// 32-tile runs per wave) and the mapping is not forced to "tile"; 8192^2
+// with sums and a uint8 reconstruction 74.3-74.8 us against 78.4 for the
+// tile kernel with the same sums path, without sums 67.0 against 76.8
+// (tools/kb_rt, profiles/r05/f/).  Otherwise the tile-per-lane kernel (IEEE
+// division, ragged widths, forced tile mapping), with its sums in the spread
+// slot's sub-slot 0 when it has one.
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s) {
     int dev = -1;
     unsigned long long* slot = nullptr;
     if (sums && hipGetDevice(&dev) == hipSuccess) slot = slot_for(dev, sums, s);
-    const bool duo = fast != 0 && recon_kind != kRtReconF32 && (!sums || slot) && g.tiles_x % 32u == 0u &&
-                     mapping_mode() != HPDCT_MAPPING_TILE;
+    const bool duo = fast != 0 && (!sums || slot) && g.tiles_x % 32u == 0u && mapping_mode() != HPDCT_MAPPING_TILE;
     hipError_t e;
     if (duo) {
-        e = launch_rt_duo(img, coef, recon_kind == kRtReconU8 ? static_cast<uint8_t*>(recon) : nullptr, slot, g, qp,
-                          fast, s);
+        e = launch_rt_duo(img, coef, recon_kind == kRtReconNone ? nullptr : recon, recon_kind, slot, g, qp, fast, s);
     } else if (slot) {
         e = tile(img, coef, recon, recon_kind, reinterpret_cast<RtSums*>(slot), g, qp, fast, s);
     } else {

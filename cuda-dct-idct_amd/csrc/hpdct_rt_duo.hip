@@ -4,9 +4,10 @@
 
 namespace hpdct {
 
-hipError_t launch_rt_duo(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread,
+hipError_t launch_rt_duo(const uint8_t* img, float* coef, void* recon, int recon_kind, unsigned long long* spread,
                          const TileGrid& g, const QParams& qp, int fast, hipStream_t s) {
-    if (recon) return rt_duo_detail::go_r<kRtReconU8>(img, coef, recon, spread, g, qp, fast, s);
+    if (recon_kind == kRtReconF32) return launch_rt_duo_f32(img, coef, recon, spread, g, qp, fast, s);
+    if (recon_kind == kRtReconU8) return rt_duo_detail::go_r<kRtReconU8>(img, coef, recon, spread, g, qp, fast, s);
     return rt_duo_detail::go_r<kRtReconNone>(img, coef, nullptr, spread, g, qp, fast, s);
 }
 

@@ -143,7 +143,7 @@ __device__ __forceinline__ void rt_duo_row_sums(uint2 w, const float (&r)[8], ui
 // the whole body ~16 VGPRs (94 against 78).
 template <bool kStats, int kQMode, int kRecon, bool kRun>
 __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, float* __restrict__ coef,
-                                            uint8_t* __restrict__ recon, const DuoAddr& a, uint32_t h,
+                                            void* __restrict__ recon, const DuoAddr& a, uint32_t h,
                                             const float (&tab)[2][64], float4* __restrict__ slots, f32x2& acc_f2,
                                             uint32_t& acc_xx, uint32_t& acc_xr, uint32_t& acc_rr) {
     constexpr bool kNT = true;
@@ -265,7 +265,23 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
         const uint2 r8 = make_uint2(pack_u8x4(r[0], r[1], r[2], r[3]), pack_u8x4(r[4], r[5], r[6], r[7]));
         if constexpr (kStats) rt_duo_row_sums(raw[k], r, r8, acc_f2, acc_xx, acc_xr, acc_rr);
         if constexpr (kRecon == kRtReconU8) {
-            if (kRun || a.valid) st<kNT>(reinterpret_cast<uint2*>(recon + a.base + a.off(2u * k + h)), r8);
+            if (kRun || a.valid)
+                st<kNT>(reinterpret_cast<uint2*>(static_cast<uint8_t*>(recon) + a.base + a.off(2u * k + h)), r8);
+        } else if constexpr (kRecon == kRtReconF32) {
+            // fp32 R + 128 (the reference's float output), re-staged like the
+            // coefficient rows: 1 KiB contiguous per store instruction
+            if constexpr (kRun) {
+                float4* const slot = slots + (k & 1) * 128;
+                slot[2u * lane] = make_float4(r[0], r[1], r[2], r[3]);
+                slot[2u * lane + 1u] = make_float4(r[4], r[5], r[6], r[7]);
+                const float4 lo4 = slot[lane], hi4 = slot[64u + lane];
+                char* const dst = reinterpret_cast<char*>(static_cast<float*>(recon) + a.base);
+                const uint32_t o_lo = (2u * k * a.width + 4u * lane) * 4u, o_hi = o_lo + a.width * 4u;
+                st<kNT>(reinterpret_cast<float4*>(dst + o_lo), lo4);
+                st<kNT>(reinterpret_cast<float4*>(dst + o_hi), hi4);
+            } else {
+                if (a.valid) store_row<kNT>(static_cast<float*>(recon) + a.base + a.off(2u * k + h), r);
+            }
         }
     });
     if constexpr (kStats) {
@@ -275,7 +291,7 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
 
 // kQMode 1: the verified 3-op quotient at every position; 2: the default JPEG
 // table's short forms where both of an instruction's positions have one.
-// kRecon: kRtReconU8 or kRtReconNone.  kWaves: waves per SIMD the register
+// kRecon: kRtReconU8, kRtReconF32 or kRtReconNone.  kWaves: waves per SIMD the register
 // allocation must allow.
 // Sums epilogue.  One 64-bit atomic add per field per workgroup into ONE
 // struct serialises once the workgroups are many: 8192^2 in 256-thread duo
@@ -298,10 +314,9 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
 template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSets = 1,
           int kSpreadN = kRtSpread>
 __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void roundtrip_duo_kernel(
-    const uint8_t* __restrict__ img, float* __restrict__ coef, uint8_t* __restrict__ recon, RtSums* __restrict__ sums,
+    const uint8_t* __restrict__ img, float* __restrict__ coef, void* __restrict__ recon, RtSums* __restrict__ sums,
     TileGrid g, QParams qp) {
     static_assert(kQMode == 1 || kQMode == 2, "duo round trip: verified quotient only");
-    static_assert(kRecon == kRtReconU8 || kRecon == kRtReconNone, "duo round trip: uint8 reconstruction");
     constexpr uint32_t kW = kBlockT / 64u;
 
     // Q and RN(1/Q) for per-lane reads (the lanes of one instruction use rows 2k and 2k+1)
@@ -383,7 +398,7 @@ namespace rt_duo_detail {
 // 36.9 against 31.9 us with sums, profiles/r05/b/kb_rt_ragged.log).
 constexpr int kDuoRtBlock = 256, kDuoRtWaves = 6;
 template <bool kStats, int kQMode, int kRecon>
-hipError_t go(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread, const TileGrid& g,
+hipError_t go(const uint8_t* img, float* coef, void* recon, unsigned long long* spread, const TileGrid& g,
               const QParams& qp, hipStream_t s) {
     hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, kQMode, kRecon, true, kDuoRtBlock, kDuoRtWaves>),
                        roundtrip_duo_grid(g, kDuoRtBlock), dim3(kDuoRtBlock), 0, s, img, coef, recon,
@@ -391,7 +406,7 @@ hipError_t go(const uint8_t* img, float* coef, uint8_t* recon, unsigned long lon
     return hipGetLastError();
 }
 template <int kRecon>
-hipError_t go_r(const uint8_t* img, float* coef, uint8_t* recon, unsigned long long* spread, const TileGrid& g,
+hipError_t go_r(const uint8_t* img, float* coef, void* recon, unsigned long long* spread, const TileGrid& g,
                 const QParams& qp, int qmode, hipStream_t s) {
     if (spread) {
         return qmode == 2 ? go<true, 2, kRecon>(img, coef, recon, spread, g, qp, s)
