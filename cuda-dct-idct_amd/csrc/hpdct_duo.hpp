@@ -131,10 +131,12 @@ __global__ __launch_bounds__(kBlock<kVar>) void fdct_duo_kernel(const float* __r
         x[i][0] = v.x - shift, x[i][1] = v.y - shift, x[i][2] = v.z - shift, x[i][3] = v.w - shift;
     });
     if constexpr (kWriteback) {  // X - 128 left in the caller's image (main_newAppr.cu:273)
+        // non-temporal like every output plane (the row-first kernel's write-back too)
+        constexpr bool kNT = (kVar & kVarNT) != 0;
         if (p.valid)
             unroll<8>([&](auto i) {
-                *reinterpret_cast<float4*>(shifted + p.base + i * g.width + 4u * h) =
-                    make_float4(x[i][0], x[i][1], x[i][2], x[i][3]);
+                st<kNT>(reinterpret_cast<float4*>(shifted + p.base + i * g.width + 4u * h),
+                        make_float4(x[i][0], x[i][1], x[i][2], x[i][3]));
             });
     }
     float pp[8][4];

@@ -57,7 +57,7 @@ KERNELS = {
     # round 5: the two-lanes-per-tile kernel (hpdct_rt_duo.hpp) is what hpdct_roundtrip_u8 launches at 8192^2
     "roundtrip_u8_f32_u8_sums": ("roundtrip_duo_kernel<true, 2, 1, true, 256, 6", (), "x2", {"x4nt": 4, "x2nt": 1}, 1, 5),
     # the drop-in surface (bench.py extras "dropin": what hpdct_compat.cpp launches)
-    "compat_fwd_f32_wb": ("fdct_duo_kernel<true, false, true", (), "x4", {"x4nt": 4, "x4plain": 4}, 4, 8),
+    "compat_fwd_f32_wb": ("fdct_duo_kernel<true, false, true", (), "x4", "x4nt", 4, 8),  # write-back NT since r05
     "compat_inv_f32": ("idct_duo_kernel<true, false", ("unsigned char",), "x4", "x4nt", 4, 4),
     "compat_fwd_rowfirst_wb": ("rowfirst_duo_kernel<false, true, false, true", (), "x4", "x4nt", 4, 8),
     "compat_inv_rowfirst_wb": ("rowfirst_duo_kernel<true, true, false, true", (), "x4", "x4nt", 4, 8),
