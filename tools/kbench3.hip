@@ -455,6 +455,15 @@ int main(int argc, char** argv) {
         {"lim", "pat 1-wave WGs, cap 7 w/cu", pat_grid_cap1_go<7>, 5, 4, false},
         {"lim", "pat 1-wave WGs, uncapped", pat_grid_cap1_go<0>, 5, 4, false},
         {"lim1", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        // the headline without the LDS re-staging of its rows (each lane stores its tile's 32-B rows directly):
+        // at <= 7 waves per CU a wave's 8 LDS round trips are poorly hidden
+        {"nolds", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"nolds", "fwd u8->f32 no LDS staging, cap 7 w/cu", prod_f32_fwd_cap<(530457u & ~8u), 7>, 5, 4, true},
+        {"nolds", "fwd u8->f32 no LDS staging, cap 8 w/cu", prod_f32_fwd_cap<(530457u & ~8u), 8>, 5, 4, true},
+        {"nolds", "fwd u8->f32 no LDS staging, cap 10 w/cu", prod_f32_fwd_cap<(530457u & ~8u), 10>, 5, 4, true},
+        {"nolds", "fwd u8->f32 no LDS staging, cap 12 w/cu", prod_f32_fwd_cap<(530457u & ~8u), 12>, 5, 4, true},
+        {"nolds", "fwd u8->f32 product kernel, cap 7 w/cu again", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"nolds", "fwd u8->f32 no LDS staging, cap 7 w/cu again", prod_f32_fwd_cap<(530457u & ~8u), 7>, 5, 4, true},
         {"lim4", "pat 1-wave WGs, cap 4 w/cu", pat_grid_cap1_go<4>, 5, 4, false},
         {"lim7", "pat 1-wave WGs, cap 7 w/cu", pat_grid_cap1_go<7>, 5, 4, false},
         {"occpat", "pat one set per wave (grid)", pat_grid_go, 5, 4, false},
