@@ -51,6 +51,10 @@ enum : unsigned {
                               // kVarFastDiv): per position the 3-op form F or H where it is proven exact
                               // below that position's |C| bound, the 6-op form elsewhere
                               // (hpdct_quant_forms.h, tests/tools/verify_quant_pos.c)
+    kVarHoistRun = 1u << 20,  // packed u8 -> fp32 forward (the capped headline kernel): the whole-run test
+                              // (split == 64) taken once per set, two straight-line copies of the body, and in
+                              // the whole-run copy each row's re-staged stores issued one row later, after the
+                              // next row's LDS writes (tools/kbench3 group hoist: 56.5 against 57.4-57.7 us)
     kVarStraddle = 1u << 30,  // fp32 LDS-staged rows: a 64-tile set that straddles two tile rows (width not a
                               // multiple of 512 px) stores two contiguous runs per instruction instead of
                               // 32 B per lane; launched only for such widths (the branch costs the
@@ -569,6 +573,13 @@ __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img
     float4* const slots = wave_slots<kVar>();
     const RowSink<kVar, float> sink{reinterpret_cast<float*>(out), g.width, slots};
     walk_sets<kVar>(img, g, slots, [&](const RawTile<uint8_t>& raw, const TilePos& p, uint32_t ok, uint64_t seg) {
+      auto work = [&](auto whole_run) {
+        // whole runs: each row's two re-staged float4 are stored one row later,
+        // so the LDS read's latency hides under the next row's arithmetic
+        float4 pend_a = make_float4(0.f, 0.f, 0.f, 0.f), pend_b = pend_a;
+        constexpr bool kNTs = (kVar & kVarNT) != 0;
+        const uint32_t lane = threadIdx.x & 63u;
+        float* const run0 = reinterpret_cast<float*>(out) + seg;
         float xs[8][8];
         raw.to_float(xs, 0.0f);
         f32x2 x2[8][4];  // X - 128, exact (integers)
@@ -589,9 +600,35 @@ __device__ __forceinline__ void fdct_packed_body(const uint8_t* __restrict__ img
                 st<(kVar & kVarNT) != 0>(reinterpret_cast<uint2*>(out + p.base + v * g.width), w);
             } else {
                 unroll<8>([&](auto u) { c[u] = __builtin_truncf(c[u]); });
-                sink(v, p, ok, seg, c);
+                if constexpr (decltype(whole_run)::value) {
+                    float4* const slot = slots + (v & 1) * 128;
+                    slot[2 * lane] = make_float4(c[0], c[1], c[2], c[3]);
+                    slot[2 * lane + 1] = make_float4(c[4], c[5], c[6], c[7]);
+                    const float4 a = slot[lane], b = slot[64 + lane];
+                    if constexpr (v > 0) {
+                        st_at<kNTs>(run0 + (v - 1) * g.width, 16u * lane, pend_a);
+                        st_at<kNTs>(run0 + (v - 1) * g.width, 16u * (64u + lane), pend_b);
+                    }
+                    pend_a = a, pend_b = b;
+                } else {
+                    sink(v, p, ok, seg, c);
+                }
             }
         });
+        if constexpr (decltype(whole_run)::value) {
+            st_at<kNTs>(run0 + 7u * g.width, 16u * lane, pend_a);
+            st_at<kNTs>(run0 + 7u * g.width, 16u * (64u + lane), pend_b);
+        }
+      };
+      if constexpr ((kVar & kVarHoistRun) != 0 && (kVar & kVarLdsStore) != 0 && std::is_same_v<TOut, float>) {
+          if (ok == 64u) {
+              work(std::true_type{});
+          } else {
+              work(std::false_type{});
+          }
+      } else {
+          work(std::false_type{});
+      }
     });
 }
 

@@ -173,8 +173,11 @@ hipError_t fdct_tile_go(const TIn* img, TOut* out, float* shifted, const TileGri
         if (sets_per_cu <= kBigWgSetsPerCU)
             return fdct_go<(kV & ~(3u << 12)) | (3u << 12), TIn, TOut, kQuant, kBuiltinT, kWriteback>(
                 img, out, shifted, g, t_dev, q, shift, s);
-        return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg | kVarPacked, TIn, TOut, kQuant, kBuiltinT, kWriteback>(
-            img, out, shifted, g, t_dev, q, shift, s, kF32CapWavesPerCU);
+        // kVarHoistRun (round 5): the whole-run test once per set and each
+        // row's store one row later: 56.5 against 57.4-57.7 us at 8192^2,
+        // bit-exact (tools/kbench3 group hoist, profiles/r05/o/)
+        return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg | kVarPacked | kVarHoistRun, TIn, TOut, kQuant, kBuiltinT,
+                       kWriteback>(img, out, shifted, g, t_dev, q, shift, s, kF32CapWavesPerCU);
     }
     if constexpr (std::is_same_v<TIn, uint8_t> && std::is_same_v<TOut, int8_t> && (kV & kVarJpegQ) != 0u) {
         return fdct_go<(kV & ~(3u << 12)) | kOneWaveWg, TIn, TOut, kQuant, kBuiltinT, kWriteback>(

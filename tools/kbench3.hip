@@ -455,6 +455,13 @@ int main(int argc, char** argv) {
         {"lim", "pat 1-wave WGs, cap 7 w/cu", pat_grid_cap1_go<7>, 5, 4, false},
         {"lim", "pat 1-wave WGs, uncapped", pat_grid_cap1_go<0>, 5, 4, false},
         {"lim1", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        // the whole-run test hoisted out of the per-row stores (two straight-line body copies)
+        {"hoist", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"hoist", "fwd u8->f32 hoisted run test, cap 7 w/cu", prod_f32_fwd_cap<(530457u | kVarHoistRun), 7>, 5, 4, true},
+        {"hoist", "fwd u8->f32 hoisted run test, cap 6 w/cu", prod_f32_fwd_cap<(530457u | kVarHoistRun), 6>, 5, 4, true},
+        {"hoist", "fwd u8->f32 hoisted run test, cap 8 w/cu", prod_f32_fwd_cap<(530457u | kVarHoistRun), 8>, 5, 4, true},
+        {"hoist", "fwd u8->f32 product kernel, cap 7 w/cu again", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
+        {"hoist", "fwd u8->f32 hoisted run test, cap 7 w/cu again", prod_f32_fwd_cap<(530457u | kVarHoistRun), 7>, 5, 4, true},
         // the headline without the LDS re-staging of its rows (each lane stores its tile's 32-B rows directly):
         // at <= 7 waves per CU a wave's 8 LDS round trips are poorly hidden
         {"nolds", "fwd u8->f32 product kernel, cap 7 w/cu", prod_f32_fwd_cap<530457u, 7>, 5, 4, true},
