@@ -52,6 +52,9 @@ EXTRA_WARM_S = 0.02            # untimed steady-state lead-in per extra (>= 20 m
 HEADLINE_LEAD_S = 0.02         # the headline's warm-up reaches at least this much wall time
 MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MI355X_MICROARCH.md)
 INPUT_FOOTPRINT = 4 * MALL_BYTES  # rotating inputs must total at least this
+WATCHDOG_EXIT = 3              # exit code when the extras watchdog fired (headline line printed)
+CEIL_CAPS = (0, 4, 8, 12, 16)  # residency caps (waves per CU) the copy ceilings are timed at; 0 = none
+DONE_FRAC = 0.9                # a kernel at >= this fraction of its copy ceiling is "done"
 
 
 def sets_for(input_bytes: int, minimum: int = 2) -> int:
@@ -346,7 +349,10 @@ def main():
                     line["extras"] = {"error": f"extras did not finish within {args.extras_timeout_s:.0f} s "
                                                "(watchdog); headline measured before them"}
                     print(json.dumps(line), file=json_out, flush=True)
-                os._exit(0)
+                # non-zero: a hang in C4/C5 (a stuck RCCL gather, say) must not
+                # read as a successful run to a caller that checks the exit
+                # code; the headline line is already out
+                os._exit(WATCHDOG_EXIT)
 
             watchdog = threading.Timer(args.extras_timeout_s, _extras_timed_out)
             watchdog.daemon = True
@@ -359,6 +365,12 @@ def main():
         if watchdog is not None:
             watchdog.cancel()
         result["extras"] = extras
+        hc = extras.get("headline_ceiling")
+        if hc:
+            # the headline kernel against the copy of its own bytes (1 B in,
+            # 4 B NT out), beside its fraction of the 8 TB/s spec
+            result["roofline"]["copy_ceiling_us"] = hc["us"]
+            result["roofline"]["frac_of_copy_ceiling"] = round(hc["us"] / (kavg * 1e3), 4)
         c4 = extras.get("c4", {})
         # the north_star row-shard figures (C4, 16384^2 over the ranks), top level
         for key in ("compute_speedup_vs_1gpu", "predicted_compute_speedup_2", "predicted_compute_speedup_4",
@@ -368,6 +380,11 @@ def main():
                 result["c4_" + key] = c4[key]
         if "compute_ms_max_rank" in c4:
             result["c4_compute_ms_max_rank"] = c4["compute_ms_max_rank"]
+        # who took part in the C4 gather: the RCCL
+        # communicator's size and the process group's, both == n_gpus
+        for key in ("rccl_nranks", "pg_world", "gather_bytes_to_root", "gather_bytes_expected"):
+            if key in c4:
+                result["c4_" + key] = c4[key]
 
     # ------------------------------------------------------------ CPU baseline
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -407,27 +424,76 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
             torch.cuda.synchronize()
         return timed_loop0(calls, steps, 0)
 
+    steps = EXTRA_STEPS
+    ceilings = {}
+
+    scratch = {}
+
+    def planes(dtype, which):
+        """two scratch output planes per (dtype, output slot): the ceilings
+        never write over a kernel's inputs or outputs"""
+        if (dtype, which) not in scratch:
+            scratch[(dtype, which)] = [torch.empty((n, n), dtype=dtype, device=dev) for _ in range(2)]
+        return scratch[(dtype, which)]
+
+    def ceiling(srcs, o0_dtype, o1_dtype=None):
+        """The copy ceiling of a kernel: hpdct_copy_ceiling
+        moving the kernel's own bytes per pixel, reading the kernel's rotating
+        inputs and writing two scratch planes per output (as the inverse and
+        round-trip legs write two), timed like the kernel at each residency cap
+        of CEIL_CAPS; the fastest is the ceiling.  One measurement per byte
+        pattern (in, out0, out1 bytes), shared by the kernels that move it."""
+        size = {torch.uint8: 1, torch.int8: 1, torch.float32: 4}
+        key = (size[srcs[0].dtype], size[o0_dtype], size[o1_dtype] if o1_dtype else 0)
+        if key not in ceilings:
+            o0s = planes(o0_dtype, 0)
+            o1s = planes(o1_dtype, 1) if o1_dtype else None
+            by = {}
+            for cap in CEIL_CAPS:
+                calls = [hpdct.bind_copy_ceiling(srcs[i], o0s[i % 2], o1s[i % 2] if o1s else None,
+                                                 cap_waves=cap, stream=stream) for i in range(len(srcs))]
+                rms, _, _ = timed_loop(calls, steps, 5)
+                by[str(cap)] = round(rms / steps * 1e3, 2)
+            best = min(by, key=by.get)
+            ceilings[key] = {"us": by[best], "cap_waves": int(best), "by_cap_us": by,
+                             "bytes_per_px": sum(key), "pattern": f"{key[0]} B in, {key[1]}"
+                                                                  + (f" + {key[2]}" if key[2] else "") + " B out"}
+        return ceilings[key]
+
+    def with_ceiling(line, ceil):
+        """ceiling_us / frac_of_ceiling beside hbm_frac, and the kernel's status:
+        done at >= DONE_FRAC of the copy of its own bytes"""
+        line["ceiling_us"] = ceil["us"]
+        line["frac_of_ceiling"] = round(ceil["us"] / line["kernel_us_avg"], 4)
+        line["ceiling"] = ceil
+        line["status"] = "done" if line["frac_of_ceiling"] >= DONE_FRAC else "open"
+        return line
+
     if True:
-        steps = EXTRA_STEPS
         # fp32 in -> fp32 out (the reference's own data types; compat kernel)
         f32_in = [imgs[s].float() for s in range(args.sets)]
         f32_out = outs[:len(f32_in)]
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, stream=stream) for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_f32_f32_runtimeT"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world,
-                                               "fdct_f32_f32_duo_runtimeT", n)
+        extras["fwd_f32_f32_runtimeT"] = with_ceiling(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world, "fdct_f32_f32_duo_runtimeT", n),
+            ceiling(f32_in, torch.float32))
+        # the headline's own copy ceiling (1 B in, 4 B out), beside its roofline
+        extras["headline_ceiling"] = ceiling(imgs, torch.float32)
         # u8 -> int8 wire format
         i8 = [torch.empty((n, n), dtype=torch.int8, device=dev) for _ in range(args.sets)]
         calls = [hpdct.bind("fwd", imgs[s], i8[s], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_u8_i8"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world, "fdct_u8_i8", n)
+        extras["fwd_u8_i8"] = with_ceiling(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world, "fdct_u8_i8", n), ceiling(imgs, torch.int8))
         # inverse fp32 -> fp32 (idct_all_blocks_cuda's data path)
         rec = [torch.empty((n, n), dtype=torch.float32, device=dev) for _ in range(2)]
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world,
-                                      "idct_f32_f32_duo", n)
+        extras["inv_f32_f32"] = with_ceiling(
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world, "idct_f32_f32_duo", n),
+            ceiling(outs, torch.float32))
         # the drop-in surface: exactly what the compat entry points launch
         # (hpdct_compat.cpp), i.e. what a caller of the reference's functions
         # gets: fp32 planes, the caller's T, and the reference's in-place side
@@ -440,27 +506,30 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                  for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["dct_all_blocks_cuda"] = dict(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_f32_wb", n),
+            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world,
+                               "compat_fwd_f32_wb", n), ceiling(f32_in, torch.float32, torch.float32)),
             launches="fdct_duo_kernel<quant, runtime T, writeback>",
             bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["idct_all_blocks_cuda"] = dict(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv"], world, "compat_inv_f32", n),
+            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv"], world, "compat_inv_f32",
+                               n), ceiling(outs, torch.float32)),
             launches="idct_duo_kernel<dequant, runtime T>", bytes_note="4 B read + 4 B written")
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, writeback_shift=True, row_first=True,
                             stream=stream) for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["dct_all_blocks (cublasDCTv2)"] = dict(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_rowfirst_wb", n),
+            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world,
+                               "compat_fwd_rowfirst_wb", n), ceiling(f32_in, torch.float32, torch.float32)),
             launches="rowfirst_duo_kernel<forward, quant, runtime T, writeback>",
             bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, row_first=True, writeback_dequant=True,
                             stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["idct_all_blocks (cublasDCTv2)"] = dict(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv_wb"], world, "compat_inv_rowfirst_wb",
-                  n),
+            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv_wb"], world,
+                               "compat_inv_rowfirst_wb", n), ceiling(outs, torch.float32, torch.float32)),
             launches="rowfirst_duo_kernel<inverse, dequant, runtime T, writeback>",
             bytes_note="4 B read + 4 B pixels + 4 B q*Q written back")
         extras["dropin"] = dropin
@@ -558,6 +627,8 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         qa = hpdct.quality_from_sums(hpdct.sums_from_buffer(ring[0]), px)
         k2 = np.array([acc_ms])
         rms2 = acc_ms * steps
+        c3_ceil_u8 = ceiling(imgs, torch.float32, torch.uint8)
+        c3_ceil_f32 = ceiling(imgs, torch.float32, torch.float32)
         # the device sums against torch's on the two-kernel output: the integer
         # fields exactly (double is exact below 2^53)
         sums_exact = sums_one["sse_u8"] == int(se8) and sums_one["sum_x2"] == int(sx)
@@ -566,16 +637,18 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
             "two_kernels": {"ms_per_frame": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
                             "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
-            "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums", n),
+            "one_pass": dict(with_ceiling(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums",
+                                                n), c3_ceil_u8),
                              quality_from_device_sums=qd, sums_exact_vs_two_kernels=sums_exact,
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums in one "
                                   "pass (the round trip + a one-wave kernel that moves the sums from the library's "
                                   "slot over the caller's struct); bit-identical to the two kernels"),
-            "one_pass_f32_recon": dict(_line(px, f32_ms, float(kf.mean()), 9, world),
+            "one_pass_f32_recon": dict(with_ceiling(_line(px, f32_ms, float(kf.mean()), 9, world), c3_ceil_f32),
                                        recon_equals_two_kernels=f32_recon_exact, sums_equal_u8_pass=f32_sums_equal,
                                        note="hpdct_roundtrip_u8 with HPDCT_F32: coefficients + fp32 R+128 (the "
                                             "reference's float output) + PEEN/MSE sums in one pass"),
-            "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
+            "one_pass_sums_ring": dict(with_ceiling(_line(px, acc_ms, float(k2.mean()), 6, world), c3_ceil_u8),
+                                       quality_from_device_sums=qa,
                                        ring_sums_exact=ring_exact,
                                        note="hpdct_roundtrip_u8_accumulate, one slot per timed launch of a fresh "
                                             "caller-zeroed ring (its memset outside the timed region); the warm-up "
@@ -583,6 +656,7 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                                             "its frame's hpdct_roundtrip_u8 sums"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
         del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc, warm, warm_ring, ref_sums, want
+        scratch.clear()
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024
@@ -937,9 +1011,10 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
         return round(max_over_ranks(best), 4)
 
     peer_rows = n - rows
+    out.update(c4_identity(args.gpus, dist.get_world_size() if use_pg else 1,
+                           comm.size if comm is not None else None, rank, n, rows))
     forward(y)
     out["gather_ms"] = timed(lambda: gather(y, frame))
-    out["gather_bytes_to_root"] = peer_rows * n * 4 if rank == 0 else None
     forward_i8()
     out["gather_decode_int8_ms"] = timed(gather_i8)
     out["gather_int8_bytes_to_root"] = peer_rows * n if rank == 0 else None
@@ -993,6 +1068,31 @@ def _c4(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ra
         comm.destroy()
     del x, y, y8, frame, frame8, own_f32
     torch.cuda.empty_cache()
+    return out
+
+
+def c4_identity(gpus, pg_world, rccl_nranks, rank, n, rows):
+    """Who takes part in the C4 gather, for the line: the
+    process group's size (`pg_world`, dist.get_world_size(), 1 without a
+    group) and the RCCL communicator's (`rccl_nranks`, hpdct_comm_size; None
+    when the gather is not native RCCL, e.g. the gloo rehearsal).  Both must
+    equal --gpus, or the leg fails loudly instead of reporting a gather over
+    fewer ranks.  On the root, gather_bytes_to_root is what the peers send it:
+    the frame's rows outside its own slab, fp32, i.e. (N-1)/N of the frame for
+    N ranks and equal slabs, 0 at N = 1 (the root's slab is computed in place);
+    gather_bytes_expected is that fraction of the frame's fp32 bytes."""
+    if pg_world != gpus or (rccl_nranks is not None and rccl_nranks != gpus):
+        raise RuntimeError(f"C4 gather over the wrong ranks: --gpus {gpus}, process group {pg_world}, "
+                           f"RCCL communicator {rccl_nranks}")
+    out = {"rccl_nranks": rccl_nranks, "pg_world": pg_world}
+    if rank == 0:
+        out["gather_bytes_to_root"] = (n - rows) * n * 4
+        out["gather_bytes_expected"] = n * n * 4 * (gpus - 1) // gpus if n // 8 % gpus == 0 else None
+        if out["gather_bytes_expected"] is not None and out["gather_bytes_to_root"] != out["gather_bytes_expected"]:
+            raise RuntimeError(f"C4 root receives {out['gather_bytes_to_root']} B, expected "
+                               f"{out['gather_bytes_expected']} B for {gpus} ranks")
+    else:
+        out["gather_bytes_to_root"] = None
     return out
 
 

@@ -233,9 +233,12 @@ hpdct_status gather(hpdct_comm comm, const void* d_slab, void* d_frame, hpdct_dt
     const hpdct::dist::Geometry geo{{height, width, static_cast<int64_t>(type), root}};
 
     Pending p{comm, {}, static_cast<const char*>(d_slab), static_cast<char*>(d_frame), s, {}};
-    // one rank whose slab already sits in the frame, or is not gathered: nothing moves
-    const RootSlab eff = own == RootSlab::kCopy && d_frame == d_slab ? RootSlab::kInPlace : own;
-    p.plan = hpdct::dist::gather_plan(height, width, elem_size(type), comm->size, root, comm->rank, eff);
+    // the root's slab is in place only when it sits at ITS rows of the frame
+    // (frame + first * row bytes); a slab at the start of the frame of a root
+    // whose rows start further down is copied
+    p.plan = hpdct::dist::gather_plan(height, width, elem_size(type), comm->size, root, comm->rank,
+                                      hpdct::dist::root_slab_mode(own, d_slab, d_frame, height, width,
+                                                                  elem_size(type), comm->size, root, comm->rank));
     if (comm->rank == root && own == RootSlab::kSkip) {
         // decode the peer rows: the slabs before the root's and after it are contiguous
         int64_t first, rows;

@@ -112,6 +112,21 @@ inline std::vector<Post> gather_plan(int64_t height, int64_t width, size_t elem,
     return plan;
 }
 
+// The mode gather_plan is called with on `rank`: a kCopy root whose slab
+// already sits at its own rows of the frame (slab == frame + first * row
+// bytes) needs no copy and posts nothing for itself, so a world-1 gather
+// posts nothing at all; a slab anywhere else, e.g. at the start of the frame
+// of a root whose first row is not 0, is copied.  Other ranks and modes pass
+// through.
+inline RootSlab root_slab_mode(RootSlab own, const void* slab, const void* frame, int64_t height, int64_t width,
+                               size_t elem, int world, int root, int rank) {
+    if (own != RootSlab::kCopy || rank != root || !slab || !frame) return own;
+    int64_t first, rows;
+    shard_rows(height, world, root, first, rows);
+    const char* at = static_cast<const char*>(frame) + static_cast<uint64_t>(first) * static_cast<uint64_t>(width) * elem;
+    return at == static_cast<const char*>(slab) ? RootSlab::kInPlace : RootSlab::kCopy;
+}
+
 // Communicators of one ncclCommInitAll (one thread, one group): the gathers
 // each of them was asked for in the group, in call order.  The round may be
 // posted only when every communicator was asked for the same sequence of

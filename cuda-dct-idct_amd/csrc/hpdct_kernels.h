@@ -83,6 +83,9 @@ hipError_t launch_rt_duo(const uint8_t* img, float* coef, void* recon, int recon
 hipError_t launch_rt_duo_f32(const uint8_t* img, float* coef, void* recon, unsigned long long* spread,
                              const TileGrid& g, const QParams& qp, int fast, hipStream_t s);
 hipError_t launch_rt_finish(RtSums* dst, unsigned long long* spread, bool accumulate, hipStream_t s);
+// the spread slot of a sums pointer back to its device's free list
+// (hpdct_roundtrip_release_sums); false when the pointer had none
+bool release_sums_slot(const void* sums);
 
 // A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch
 // device pointer pairs travel in the kernel arguments (1 KiB).
@@ -106,6 +109,10 @@ hipError_t launch_decode_i8_f32(const int8_t* in, float* out, uint64_t n, hipStr
 // hpdct_floor_probe (hpdct_probe.hip): kind 0 an empty kernel, 1 a u8 -> fp32
 // copy, both on the grid the uint8 -> fp32 forward of g launches
 hipError_t launch_floor_probe(int kind, const uint8_t* in, float* out, const TileGrid& g, hipStream_t s);
+// hpdct_copy_ceiling (hpdct_probe.hip): element bytes 1 or 4 (o1_bytes 0: no
+// second output), n a multiple of 2048, at most cap_waves resident per CU
+hipError_t launch_copy_ceiling(const void* in, int in_bytes, void* o0, int o0_bytes, void* o1, int o1_bytes,
+                               uint64_t n, uint32_t cap_waves, hipStream_t s);
 
 // hpdct_mapping in force (0 auto, 1 tile, 2 octet); hpdct_api.cpp.
 int mapping_mode();

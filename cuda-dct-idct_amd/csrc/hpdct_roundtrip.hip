@@ -3,6 +3,7 @@
 // kernel of hpdct_roundtrip.hpp) and where its quality sums go.
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "hpdct.h"
 #include "hpdct_roundtrip.hpp"
@@ -10,20 +11,23 @@
 namespace hpdct {
 namespace {
 
-// Spread slots for the sums (kRtSpread sub-slots, kRtSpreadBytes each), one
-// per (device, caller's sums pointer), handed out from zeroed chunks and never
-// returned: the round trip adds into the slot and rt_spread_finish_kernel
-// folds it into the caller's struct, leaving it zero for the next launch with
-// that pointer.  Launches with one sums pointer are ordered (one stream, or
-// one graph) or race on the caller's struct anyway, so they may share its
-// slot.  nullptr when a new chunk would be needed inside a stream capture, or
-// past kMaxSlots pointers on a device: the launch then takes the tile kernel
-// with a memset of *sums (overwrite) or atomics into *sums (accumulate).
+// Spread slots for the sums (kRtSpread sub-slots, kRtSpreadBytes = 16 KiB
+// each), one per (device, caller's sums pointer), handed out from zeroed
+// chunks: the round trip adds into the slot and rt_spread_finish_kernel folds
+// it into the caller's struct, leaving it zero for the next launch with that
+// pointer.  Launches with one sums pointer share its slot; the fold is atomic,
+// so accumulate launches on different streams lose nothing.  A
+// slot stays with its pointer until hpdct_roundtrip_release_sums returns it
+// to the device's free list.  nullptr when a new chunk would be needed inside
+// a stream capture, or past kMaxSlots live pointers on a device (64 MiB of
+// slots): the launch then takes the tile kernel with a memset of *sums
+// (overwrite) or atomics into *sums (accumulate).
 constexpr size_t kSlotChunk = 256;  // 256 x 16 KiB = 4 MiB per allocation
-constexpr size_t kMaxSlots = size_t(1) << 14;
+constexpr size_t kMaxSlots = size_t(1) << 12;
 
 struct DeviceSlots {
     std::map<const void*, unsigned long long*> by_sums;
+    std::vector<unsigned long long*> free;  // released slots (zero)
     unsigned char* chunk = nullptr;
     size_t used = kSlotChunk;
     hipStream_t zero_stream = nullptr;
@@ -37,6 +41,12 @@ unsigned long long* slot_for(int dev, const void* sums, hipStream_t s) {
     DeviceSlots& d = g_slots[dev];
     auto it = d.by_sums.find(sums);
     if (it != d.by_sums.end()) return it->second;
+    if (!d.free.empty()) {
+        unsigned long long* const slot = d.free.back();
+        d.free.pop_back();
+        d.by_sums.emplace(sums, slot);
+        return slot;
+    }
     if (d.by_sums.size() >= kMaxSlots) return nullptr;
     if (d.used == kSlotChunk) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -80,6 +90,28 @@ void recover_slot(int dev, const void* sums, unsigned long long* slot, hipStream
     g_slots[dev].by_sums.erase(sums);
 }
 
+}  // namespace
+
+// hpdct_roundtrip_release_sums: the slot of `sums` (on whichever device holds
+// one) back to that device's free list.  The caller guarantees no launch with
+// that pointer is still in flight, so the slot is zero (each fold leaves it
+// so).  Returns whether the pointer had a slot.
+bool release_sums_slot(const void* sums) {
+    std::lock_guard<std::mutex> lock(g_slot_mutex);
+    bool found = false;
+    for (auto& kv : g_slots) {
+        DeviceSlots& d = kv.second;
+        auto it = d.by_sums.find(sums);
+        if (it == d.by_sums.end()) continue;
+        d.free.push_back(it->second);
+        d.by_sums.erase(it);
+        found = true;
+    }
+    return found;
+}
+
+namespace {
+
 hipError_t tile(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums, const TileGrid& g,
                 const QParams& qp, int fast, hipStream_t s) {
     switch (recon_kind) {
@@ -99,13 +131,17 @@ hipError_t tile(const uint8_t* img, float* coef, void* recon, int recon_kind, Rt
 // tile kernel with the same sums path, without sums 67.0 against 76.8
 // (tools/kb_rt, profiles/r05/f/).  Otherwise the tile-per-lane kernel (IEEE
 // division, ragged widths, forced tile mapping), with its sums in the spread
-// slot's sub-slot 0 when it has one.
+// slot's sub-slot 0 when it has one.  The duo kernel addresses a wave's rows
+// with 32-bit byte offsets from the wave's base (DuoAddr, 2 k width + 4 lane
+// fp32 words), which stay below 2^32 for widths below 2^22 pixels; wider
+// frames take the tile kernel.
 hipError_t launch_roundtrip(const uint8_t* img, float* coef, void* recon, int recon_kind, RtSums* sums,
                             const TileGrid& g, const QParams& qp, int fast, bool zero_sums, hipStream_t s) {
     int dev = -1;
     unsigned long long* slot = nullptr;
     if (sums && hipGetDevice(&dev) == hipSuccess) slot = slot_for(dev, sums, s);
-    const bool duo = fast != 0 && (!sums || slot) && g.tiles_x % 32u == 0u && mapping_mode() != HPDCT_MAPPING_TILE;
+    const bool duo = fast != 0 && (!sums || slot) && g.tiles_x % 32u == 0u && g.width < (uint64_t(1) << 22) &&
+                     mapping_mode() != HPDCT_MAPPING_TILE;
     hipError_t e;
     if (duo) {
         e = launch_rt_duo(img, coef, recon_kind == kRtReconNone ? nullptr : recon, recon_kind, slot, g, qp, fast, s);

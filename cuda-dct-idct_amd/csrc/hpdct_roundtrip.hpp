@@ -280,12 +280,19 @@ __global__ __launch_bounds__(kBlock, kRtWaves<kRecon>) void roundtrip_kernel(con
 }
 
 // Folds the kRtSpread sub-slots of a spread slot into *dst (overwriting it,
-// or adding to it when accumulate) and zeroes them: one wave, lane i reads
+// or adding to it when accumulate) and zeroes them: one wave, lane i takes
 // sub-slot i.  Next on the stream after a round trip that added into the slot
 // (hpdct_roundtrip_u8 and _accumulate, round 5).  The one-wave kernel costs
 // less than the memset it replaced (round 4: 77.6 us per 8192^2 launch against
 // 79.3 with a memset of the caller's struct before the kernel,
 // profiles/r04/j/kb3_rtring_8192.log).
+// Every step is atomic: each sub-slot word is taken and zeroed by
+// one atomic exchange, and an accumulate adds into *dst with atomic adds.  So
+// two accumulate launches with one sums pointer on different streams (one
+// slot, two round trips and two folds in flight) lose nothing: whatever one
+// fold takes of the other launch's partial sums the other fold no longer
+// finds, and both folds' adds land.  An overwrite is a plain store: two
+// overwrites of one struct in flight race by definition.
 template <int kN = kRtSpread>
 __global__ __launch_bounds__(64) void rt_spread_finish_kernel(RtSums* __restrict__ dst,
                                                               unsigned long long* __restrict__ slot, int accumulate) {
@@ -293,9 +300,8 @@ __global__ __launch_bounds__(64) void rt_spread_finish_kernel(RtSums* __restrict
     unsigned long long v[3] = {0ull, 0ull, 0ull}, bad[3] = {0ull, 0ull, 0ull};
     for (uint32_t k = l; k < static_cast<uint32_t>(kN); k += 64u) {
         unroll<3>([&](auto f) {
-            const unsigned long long x = slot[k * kRtSpreadStride + f];
+            const unsigned long long x = atomicExch(&slot[k * kRtSpreadStride + f], 0ull);
             v[f] += x & ~kRtSseF32Invalid, bad[f] |= x & kRtSseF32Invalid;
-            slot[k * kRtSpreadStride + f] = 0ull;
         });
     }
     unroll<3>([&](auto f) {
@@ -303,9 +309,12 @@ __global__ __launch_bounds__(64) void rt_spread_finish_kernel(RtSums* __restrict
         const bool flagged = __builtin_amdgcn_ballot_w64(bad[f] != 0ull) != 0ull;
         if (l == 0u) {
             auto* const d = reinterpret_cast<unsigned long long*>(dst) + f;
-            unsigned long long out = accumulate ? *d + sum : sum;
-            if (flagged) out |= kRtSseF32Invalid;
-            *d = out;
+            if (accumulate) {
+                if (sum) atomicAdd(d, sum);
+                if (flagged) atomicOr(d, kRtSseF32Invalid);
+            } else {
+                *d = flagged ? (sum | kRtSseF32Invalid) : sum;
+            }
         }
     });
 }

@@ -40,7 +40,8 @@ STATUS = {
     4: "HPDCT_ERROR_DEVICE",
 }
 
-# every symbol include/hpdct.h and include/hpdct_compat.h declare
+# every symbol include/hpdct.h, hpdct_baseline.h (A/B and measurement only)
+# and hpdct_compat.h declare
 C_SYMBOLS = [
     "hpdct_version", "hpdct_build_info", "hpdct_status_string", "hpdct_last_error_string",
     "hpdct_default_quant_table", "hpdct_default_transform",
@@ -51,7 +52,7 @@ C_SYMBOLS = [
     "hpdct_baseline_forward", "hpdct_stream_forward", "hpdct_set_mapping", "hpdct_get_mapping",
     "hpdct_roundtrip_u8", "hpdct_roundtrip_u8_accumulate", "hpdct_forward_frames",
     "hpdct_stream_create", "hpdct_stream_run", "hpdct_stream_destroy", "hpdct_decode_i8_f32",
-    "hpdct_floor_probe",
+    "hpdct_roundtrip_release_sums", "hpdct_floor_probe", "hpdct_copy_ceiling",
 ]
 MAPPINGS = {"auto": 0, "tile": 1, "octet": 2, "duo": 3}
 BASELINES = {"reference_3pass": 0, "fastappr_3pass": 1}
@@ -106,6 +107,10 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.hpdct_decode_i8_f32.restype = ctypes.c_int
     lib.hpdct_floor_probe.argtypes = [ctypes.c_int, vp, vp, i64, i64, vp]
     lib.hpdct_floor_probe.restype = ctypes.c_int
+    lib.hpdct_copy_ceiling.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, i64, ctypes.c_int, vp]
+    lib.hpdct_copy_ceiling.restype = ctypes.c_int
+    lib.hpdct_roundtrip_release_sums.argtypes = [vp]
+    lib.hpdct_roundtrip_release_sums.restype = ctypes.c_int
     lib.hpdct_status_string.restype = ctypes.c_char_p
     lib.hpdct_status_string.argtypes = [ctypes.c_int]
     lib.hpdct_last_error_string.restype = ctypes.c_char_p
@@ -644,6 +649,34 @@ def bind_floor_probe(kind: int, img=None, out=None, height: int = 0, width: int 
 
 def floor_probe(kind: int, img=None, out=None, height: int = 0, width: int = 0, stream=None) -> None:
     bind_floor_probe(kind, img, out, height, width, stream)()
+
+
+def bind_copy_ceiling(src, out0, out1=None, *, cap_waves: int = 0, stream=None):
+    """The copy ceiling of a kernel that reads src and writes out0 (and out1)
+    (hpdct_copy_ceiling, include/hpdct_baseline.h): the same bytes per pixel,
+    no arithmetic, at most cap_waves resident one-wave workgroups per CU
+    (0: no cap).  A zero-argument callable like bind().  Measurement only."""
+    n = src.numel()
+    for name, t in (("out0", out0), ("out1", out1)):
+        if t is not None:
+            _device_plane(t, name, src.device, n)
+    args = (ctypes.c_void_p(src.data_ptr()), _dtype_code(src), ctypes.c_void_p(out0.data_ptr()), _dtype_code(out0),
+            None if out1 is None else ctypes.c_void_p(out1.data_ptr()), F32 if out1 is None else _dtype_code(out1),
+            n, int(cap_waves), _stream_ptr(stream))
+    fn = load_library().hpdct_copy_ceiling
+
+    def call():
+        st = fn(*args)
+        if st:
+            _check(st)
+    return call
+
+
+def release_sums(sums_buf) -> None:
+    """Return the library's 16 KiB spread slot kept for this sums buffer
+    (hpdct_roundtrip_release_sums); call when no round trip with it is in
+    flight (e.g. before freeing a ring of sums buffers)."""
+    _check(load_library().hpdct_roundtrip_release_sums(ctypes.c_void_p(sums_buf.data_ptr())))
 
 
 # ---------------------------------------------------------------------------

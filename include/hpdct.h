@@ -142,13 +142,15 @@ hpdct_status hpdct_inverse_f32_f32(const float* d_coef, float* d_image, int64_t 
  *            kernel adds into a 16 KiB library "spread slot" kept per d_sums
  *            pointer (64 sub-slots on separate 256-B lines, so the atomics of
  *            many waves do not queue on one line; allocated zeroed on first
- *            use, 256 at a time) and a one-wave kernel then folds it into
- *            *d_sums and zeroes it: no memset before the kernel.  Without a
- *            slot (an allocation would be needed inside a stream capture, or
- *            past 16384 pointers) the launch memsets *d_sums and takes the
- *            tile-per-lane kernel.  Two launches in flight at once with the
+ *            use, 256 = 4 MiB at a time) and a one-wave kernel then folds it
+ *            into *d_sums and zeroes it: no memset before the kernel.  A slot
+ *            stays with its pointer until hpdct_roundtrip_release_sums.
+ *            Without a slot (an allocation would be needed inside a stream
+ *            capture, or 4096 pointers = 64 MiB of slots are live on the
+ *            device) the launch memsets *d_sums and takes the tile-per-lane
+ *            kernel.  Two overwriting launches in flight at once with the
  *            same d_sums on different streams race, as they would on the
- *            struct itself.
+ *            struct itself (accumulating ones do not: see below).
  * Built-in T, the library Q, level shift 128; coefficients and reconstruction
  * are bit-identical to the two separate calls.  HBM traffic per pixel: 1 B
  * read, 4 B (+1 or 4 B) written, against 10 B for the two calls.
@@ -176,10 +178,18 @@ hpdct_status hpdct_roundtrip_u8(const uint8_t* d_image, float* d_coef, void* d_r
  * kernel, which adds instead of overwriting).  A pipeline that owns a ring of
  * per-frame sums slots zeroes the ring once, with one memset for many frames,
  * and gets the same per-frame sums (or a batch total, if frames share a
- * slot). */
+ * slot).  The fold takes the slot with atomic exchanges and adds with atomic
+ * adds, so frames that share d_sums may run on different streams at once. */
 hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef, void* d_recon,
                                            hpdct_dtype recon_type, hpdct_roundtrip_sums* d_sums, int64_t height,
                                            int64_t width, void* stream);
+
+/* Return the spread slot kept for d_sums (16 KiB of device memory) to the
+ * library, e.g. before freeing a ring of per-frame sums structs.  Call it when
+ * no round trip with d_sums is in flight; a later round trip with the same
+ * pointer takes a slot again.  A pointer without a slot (or NULL) is a no-op.
+ * No reference counterpart. */
+hpdct_status hpdct_roundtrip_release_sums(const hpdct_roundtrip_sums* d_sums);
 
 /* A list of independent device frames in as few launches as possible (config
  * C2's small frames: one 1024^2 frame per launch is dispatch-bound, ~3.6 us for
@@ -238,17 +248,6 @@ hpdct_status hpdct_fill_hash_u8(uint8_t* d_out, int64_t n, uint64_t seed, int64_
  * as +0.0.  Device pointers: d_q 4-byte, d_out 16-byte aligned.  Async on
  * `stream`.  No reference counterpart (the reference has no int8 format). */
 hpdct_status hpdct_decode_i8_f32(const int8_t* d_q, float* d_out, int64_t n, void* stream);
-
-/* Measurement floors of the uint8 -> fp32 forward of a height x width frame
- * (no reference counterpart; bench.py's C2 leg): kind HPDCT_PROBE_EMPTY
- * launches an empty kernel on the grid and workgroup size that forward uses
- * (d_in, d_out unused, may be NULL), HPDCT_PROBE_COPY the same grid copying
- * the frame's bytes: d_out[i] = (float)d_in[i], 1 B read + 4 B non-temporal
- * write per pixel and no transform.  Device pointers d_in 8-byte, d_out
- * 16-byte aligned.  Async on `stream`. */
-typedef enum hpdct_probe_kind { HPDCT_PROBE_EMPTY = 0, HPDCT_PROBE_COPY = 1 } hpdct_probe_kind;
-hpdct_status hpdct_floor_probe(hpdct_probe_kind kind, const uint8_t* d_in, float* d_out, int64_t height,
-                               int64_t width, void* stream);
 
 /* Work mapping of the kernels (new; the reference has one fixed decomposition
  * per program).  Output is bit-identical in every mapping; only speed differs.

@@ -119,18 +119,26 @@ def main() -> None:
         img = O.rand_u8(n * n).reshape(n, n)
         q = O.fdct(img)
         rt = O.idct(q)
+        r8 = O.to_u8(rt)
         peen, mse = O.quality(img.astype(np.float32), rt)
-        peen8, mse8 = O.quality(img.astype(np.float32), O.to_u8(rt).astype(np.float32))
+        peen8, mse8 = O.quality(img.astype(np.float32), r8.astype(np.float32))
+        x64 = img.astype(np.int64)
         manifest["configs"][name] = {
             "input_sha256": sha(img),
             "q_f32_sha256": sha(q),
             "roundtrip_f32_sha256": sha(rt),
+            # the one-pass round trip's uint8 reconstruction (convertToUnsignedChar
+            # of R + 128) and its exact quality sums (hpdct_roundtrip_sums)
+            "roundtrip_u8_sha256": sha(r8),
+            "sum_x2": int((x64 * x64).sum()),
+            "sse_u8": int(((x64 - r8.astype(np.int64)) ** 2).sum()),
+            "sse_f32_fx": O.rt_sse_f32_fx(img, rt),
             "q_nofma_mismatches": int((O.fdct(img, nofma=True) != q).sum()),
             "q_recip_mismatches": int((O.fdct(img, recip=True) != q).sum()),
             "max_abs_q": float(np.abs(q).max()),
             "peen_f32": peen, "mse_f32": mse, "peen_u8": peen8, "mse_u8": mse8,
         }
-        del img, q, rt
+        del img, q, rt, r8, x64
 
     # glibc rand() stream: first 64 values of rand()%256 after srand(42)
     libc = ctypes.CDLL("libc.so.6")

@@ -279,6 +279,36 @@ def test_roundtrip_arguments_rejected(hp):
     assert acc(a, b, c, hp.I8, s, 8, 8, None) == 2
 
 
+def test_product_header_declares_only_the_path(hp):
+    """include/hpdct.h is the path's API; the measurement
+    probes (the C2 floors, the copy ceilings) are declared in hpdct_baseline.h
+    beside the A/B baselines, not in the product header."""
+    text = open(os.path.join(INCLUDE, "hpdct.h")).read()
+    for name in ("hpdct_floor_probe", "hpdct_copy_ceiling", "hpdct_baseline_forward", "hpdct_probe_kind"):
+        assert name not in text, name
+    base = open(os.path.join(INCLUDE, "hpdct_baseline.h")).read()
+    for name in ("hpdct_floor_probe", "hpdct_copy_ceiling", "hpdct_baseline_forward"):
+        assert name + "(" in base, name
+
+
+def test_copy_ceiling_and_release_arguments(hp):
+    """hpdct_copy_ceiling validates before any device work (no GPU here);
+    hpdct_roundtrip_release_sums of an unknown pointer or NULL is a no-op."""
+    L = hp.load_library()
+    a, b, c = ctypes.c_void_p(1 << 20), ctypes.c_void_p(1 << 30), ctypes.c_void_p(1 << 31)
+    cc = L.hpdct_copy_ceiling
+    assert cc(a, hp.U8, b, hp.F32, None, 0, 2048 * 3, -1, None) == 1        # negative cap
+    assert cc(a, hp.U8, b, hp.F32, None, 0, 2000, 0, None) == 1             # n not a multiple of 2048
+    assert cc(a, hp.U8, b, hp.F32, None, 0, 0, 0, None) == 1
+    assert cc(None, hp.U8, b, hp.F32, None, 0, 2048, 0, None) == 1
+    assert cc(a, hp.U8, ctypes.c_void_p((1 << 30) + 4), hp.F32, None, 0, 2048, 0, None) == 1  # misaligned
+    assert cc(a, hp.U8, b, hp.F32, ctypes.c_void_p((1 << 31) + 8), hp.U8, 2048, 0, None) == 1
+    assert cc(a, 7, b, hp.F32, None, 0, 2048, 0, None) == 2                  # unknown type
+    assert cc(a, hp.U8, b, hp.F32, c, 9, 2048, 0, None) == 2
+    assert L.hpdct_roundtrip_release_sums(None) == 0
+    assert L.hpdct_roundtrip_release_sums(ctypes.c_void_p(1 << 33)) == 0
+
+
 def test_forward_frames_arguments_rejected(hp):
     """hpdct_forward_frames validates the whole pointer table before any
     device work (no GPU here): shape, counts, nulls, alignment, overlaps."""

@@ -125,6 +125,14 @@ int main(int argc, char** argv) {
         printf("%s\n", clique_round_agrees(asked, failed) ? "post" : "refuse");
         return 0;
     }
+    if (argc > 1 && !strcmp(argv[1], "mode")) {
+        // mode <height> <width> <elem> <world> <root> <rank> <own> <slab byte offset into the frame>
+        static char frame[1];
+        const char* slab = frame + atoll(argv[9]);
+        printf("%d\n", (int)root_slab_mode((RootSlab)atoi(argv[8]), slab, frame, atoll(argv[2]), atoll(argv[3]),
+                                           (size_t)atoll(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7])));
+        return 0;
+    }
     return 2;
 }
 """
@@ -221,3 +229,46 @@ def test_clique_round_posts_only_when_all_agree(plan_driver):
     assert _round(plan_driver, [(False, [f32])] * 3 + [(False, [])]) == "refuse"  # one communicator missing
     assert _round(plan_driver, [(False, [f32])] * 3 + [(True, [])]) == "refuse"   # one call failed its checks
     assert _round(plan_driver, [(False, [f32])] * 2 + [(False, [(16384, 16384, 2, 1)])]) == "refuse"
+
+
+R_COPY, R_IN_PLACE, R_SKIP = 0, 1, 2  # hpdct::dist::RootSlab
+
+
+def _mode(exe, height, width, elem, world, root, rank, own, slab_off):
+    r = subprocess.run([exe, "mode"] + [str(v) for v in (height, width, elem, world, root, rank, own, slab_off)],
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    return int(r.stdout.strip())
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("elem", [4, 1])
+def test_root_slab_in_place_only_at_its_own_rows(plan_driver, world, elem):
+    """hpdct_gather_rows treats the root's slab as already
+    in place only when it sits at the root's OWN rows of the frame.  A root
+    other than 0 whose slab is the start of the frame (slab == frame) must
+    copy it to its rows, or rank 0's receive overwrites it and the root's rows
+    stay unwritten.  Every root, slab at the frame start and at its rows."""
+    height, width = 8 * 13, 8 * 5
+    for root in range(world):
+        first, _ = _shard(height, world, root)
+        at_rows = first * width * elem
+        assert _mode(plan_driver, height, width, elem, world, root, root, R_COPY, at_rows) == R_IN_PLACE  # in place
+        want_start = R_IN_PLACE if at_rows == 0 else R_COPY  # root 0: its rows ARE the frame start
+        assert _mode(plan_driver, height, width, elem, world, root, root, R_COPY, 0) == want_start
+        # the plan of a root > 0 with slab == frame copies its own rows
+        if at_rows:
+            plan = _plan(plan_driver, height, width, elem, world, root, root, R_COPY)
+            assert (COPY, root, first, _shard(height, world, root)[1], at_rows,
+                    _shard(height, world, root)[1] * width * elem) in plan
+        # skip (the int8 gather-decode) and non-root ranks pass through
+        assert _mode(plan_driver, height, width, elem, world, root, root, R_SKIP, 0) == R_SKIP
+        for rank in range(world):
+            if rank != root:
+                assert _mode(plan_driver, height, width, elem, world, root, rank, R_COPY, at_rows) == R_COPY
+
+
+def test_library_uses_root_slab_mode():
+    src = open(os.path.join(CSRC, "hpdct_dist.cpp")).read()
+    assert "hpdct::dist::root_slab_mode(own, d_slab, d_frame" in src
+    assert "d_frame == d_slab ?" not in src

@@ -120,3 +120,66 @@ def test_native_dist_rejects_bad_arguments():
     assert lib.hpdct_comm_destroy(None) == 0
     with pytest.raises(hpdct.HpdctError):
         hpdct.Comm.init_rank(1, b"x" * 10, 0, 0)
+
+
+# ---- the C4 leg's self-check of who took part (bench.c4_identity) -----------
+def _identity_worker(rank, world, port, result_path):
+    import json
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 16384
+        _, rows = shard_rows(n, world, rank)
+        # what the native RCCL leg records (communicator size == world) and
+        # the gloo rehearsal (no communicator)
+        native = bench.c4_identity(world, dist.get_world_size(), world, rank, n, rows)
+        rehearsal = bench.c4_identity(world, dist.get_world_size(), None, rank, n, rows)
+        refused = []
+        for bad in ((world + 1, dist.get_world_size(), world), (world, dist.get_world_size(), world - 1)):
+            try:
+                bench.c4_identity(bad[0], bad[1], bad[2], rank, n, rows)
+            except RuntimeError as e:
+                refused.append(str(e))
+        out = [None] * world
+        dist.all_gather_object(out, {"native": native, "rehearsal": rehearsal, "refused": len(refused)})
+        if rank == 0:
+            with open(result_path, "w") as fh:
+                json.dump(out, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c4_line_carries_the_rank_count_world2(tmp_path):
+    """the C4 leg records rccl_nranks (hpdct_comm_size) and
+    pg_world (dist.get_world_size()), fails loudly when either differs from
+    --gpus, and on the root records gather_bytes_to_root = (N-1)/N of the
+    fp32 frame: a two-rank gloo group assembles the fields the line carries."""
+    import json
+    import torch.multiprocessing as mp
+    result = tmp_path / "identity.json"
+    mp.spawn(_identity_worker, args=(2, _free_port(), str(result)), nprocs=2, join=True)
+    got = json.loads(result.read_text())
+    n = 16384
+    for rank, r in enumerate(got):
+        assert r["native"]["pg_world"] == 2 and r["native"]["rccl_nranks"] == 2
+        assert r["rehearsal"]["rccl_nranks"] is None and r["rehearsal"]["pg_world"] == 2
+        assert r["refused"] == 2
+        if rank == 0:
+            assert r["native"]["gather_bytes_to_root"] == n * n * 4 // 2 == r["native"]["gather_bytes_expected"]
+        else:
+            assert r["native"]["gather_bytes_to_root"] is None
+
+
+@pytest.mark.parametrize("world", [1, 4, 8])
+def test_c4_identity_root_bytes(world):
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 16384
+    _, rows = shard_rows(n, world, 0)
+    ident = bench.c4_identity(world, world, world, 0, n, rows)
+    assert ident["gather_bytes_to_root"] == n * n * 4 * (world - 1) // world == ident["gather_bytes_expected"]

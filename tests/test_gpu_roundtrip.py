@@ -331,28 +331,116 @@ def test_roundtrip_rejects_bad_arguments(hp, dev):
         hp.roundtrip(x, coef=buf[1:257].view(16, 16))  # misaligned coefficient plane
 
 
-def test_c3_8192_roundtrip_one_pass(hp, oracle, dev, golden):
-    """C3 at full size: coefficients and fp32 reconstruction match the golden
-    digests of the oracle; PEEN/MSE from the device sums match the golden
-    values of both reconstructions."""
+@pytest.fixture(scope="module")
+def c3_frame(oracle, dev):
+    img = oracle.rand_u8(8192 * 8192).reshape(8192, 8192)
+    return img, to_dev(img, dev)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_c3_8192_roundtrip_one_pass(hp, oracle, dev, golden, c3_frame):
+    """C3 at full size with the fp32 reconstruction: coefficients and
+    reconstruction match the golden digests of the oracle; PEEN/MSE from the
+    device sums match the golden values of both reconstructions."""
     import torch
     g = golden["configs"]["c3_8192"]
-    img = oracle.rand_u8(8192 * 8192).reshape(8192, 8192)
-    x = to_dev(img, dev)
+    img, x = c3_frame
     coef, recf, got = hp.roundtrip(x, recon_dtype=torch.float32, sums=True)
-
-    def sha(a):
-        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
-
-    assert sha(to_host(coef)) == g["q_f32_sha256"]
-    assert sha(to_host(recf)) == g["roundtrip_f32_sha256"]
+    assert _sha(to_host(coef)) == g["q_f32_sha256"]
+    assert _sha(to_host(recf)) == g["roundtrip_f32_sha256"]
     px = 8192 * 8192
     q = hp.quality_from_sums(got, px)
     assert abs(q["mse_f32"] - g["mse_f32"]) < 1e-5 * g["mse_f32"]
     assert abs(q["peen_f32_pct"] - g["peen_f32"]) < 1e-5 * g["peen_f32"]
     assert abs(q["mse_u8"] - g["mse_u8"]) < 1e-9 * g["mse_u8"]
     assert abs(q["peen_u8_pct"] - g["peen_u8"]) < 1e-9 * g["peen_u8"]
-    assert got["sum_x2"] == int((img.astype(np.int64) ** 2).sum())
+    assert got["sum_x2"] == g["sum_x2"] and got["sse_u8"] == g["sse_u8"]
+    assert got["sse_f32"] * 65536 == g["sse_f32_fx"]
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_c3_8192_benched_one_pass_u8_recon(hp, dev, golden, c3_frame, accumulate):
+    """the configuration bench.py times as
+    extras.c3_roundtrip.one_pass (and one_pass_sums_ring), at the config's
+    size: uint8 reconstruction + sums through bind_roundtrip on a side stream,
+    i.e. the two-lanes-per-tile kernel (roundtrip_duo_kernel<sums, JPEG forms,
+    u8>) and the spread-slot fold.  Coefficients, the uint8 reconstruction and
+    all three sums equal the oracle's (golden digests and exact integers,
+    tests/golden/make_golden.py), twice in a row with one sums buffer: the
+    overwrite gives the frame's sums both times (the fold leaves the slot
+    zero), accumulate twice the frame's."""
+    import torch
+    g = golden["configs"]["c3_8192"]
+    _, x = c3_frame
+    coef = torch.full((8192, 8192), float("nan"), dtype=torch.float32, device=dev)
+    rec = torch.full((8192, 8192), 7, dtype=torch.uint8, device=dev)
+    buf = torch.zeros(3, dtype=torch.int64, device=dev) if accumulate else torch.full((3,), -5, dtype=torch.int64,
+                                                                                       device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    call = hp.bind_roundtrip(x, coef, rec, buf, stream=side, accumulate=accumulate)
+    for k in (1, 2):
+        call()
+        side.synchronize()
+        got = hp.sums_from_buffer(buf)
+        m = k if accumulate else 1
+        assert got["sum_x2"] == m * g["sum_x2"] and got["sse_u8"] == m * g["sse_u8"], k
+        assert got["sse_f32"] * 65536 == m * g["sse_f32_fx"], k
+    assert _sha(to_host(coef)) == g["q_f32_sha256"]
+    assert _sha(to_host(rec)) == g["roundtrip_u8_sha256"]
+    hp.release_sums(buf)
+
+
+def test_roundtrip_accumulate_two_streams_one_sums(hp, oracle, dev):
+    """accumulate launches that share one sums buffer on
+    two streams at once (one spread slot, two round trips and two folds in
+    flight) lose nothing: the fold takes the slot with atomic exchanges and
+    adds with atomic adds.  Many launches, interleaved over two streams with
+    no ordering between them, add up to exactly n x the frame's sums."""
+    import torch
+    a = oracle.rand_u8(512 * 2048, 77).reshape(512, 2048)
+    want = expected(oracle, a)[3]
+    x = to_dev(a, dev)
+    buf = torch.zeros(3, dtype=torch.int64, device=dev)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream())
+    coefs = [torch.empty(a.shape, dtype=torch.float32, device=dev) for _ in range(2)]
+    calls = [hp.bind_roundtrip(x, coefs[i], None, buf, stream=s, accumulate=True) for i, s in enumerate((s1, s2))]
+    n = 40
+    for i in range(n):
+        calls[i % 2]()
+    torch.cuda.synchronize()
+    got = hp.sums_from_buffer(buf)
+    assert got["sum_x2"] == n * want["sum_x2"] and got["sse_u8"] == n * want["sse_u8"]
+    fx = oracle.rt_sse_f32_fx(a, oracle.idct(oracle.fdct(a)))
+    assert got["sse_f32"] * 65536 == n * fx
+    hp.release_sums(buf)
+
+
+def test_roundtrip_release_sums_reuses_slots(hp, oracle, dev):
+    """hpdct_roundtrip_release_sums: a released buffer's slot
+    goes back to the library and is handed to the next new sums pointer; every
+    buffer still gets its frame's sums, before and after."""
+    import torch
+    a = oracle.rand_u8(64 * 256, 91).reshape(64, 256)
+    want = expected(oracle, a)[3]
+    x = to_dev(a, dev)
+    coef = torch.empty(a.shape, dtype=torch.float32, device=dev)
+    for rnd in range(3):
+        bufs = [torch.full((3,), -1, dtype=torch.int64, device=dev) for _ in range(300)]
+        for b in bufs:
+            hp.bind_roundtrip(x, coef, None, b)()
+        torch.cuda.synchronize()
+        for b in bufs:
+            check_sums(hp.sums_from_buffer(b), want)
+        for b in bufs:
+            hp.release_sums(b)
+        del bufs
+    hp.release_sums(torch.zeros(3, dtype=torch.int64, device=dev))  # never used: a no-op
 
 
 @pytest.mark.parametrize("mapping", ["auto", "tile"])

@@ -45,3 +45,26 @@ def test_fastdiv_sampled_jpeg_table(tmp_path):
 def test_committed_exhaustive_logs(log, pattern):
     text = open(os.path.join(TOOLS, log)).read()
     assert re.search(pattern, text)
+
+
+def test_rt_pair_trace_reads_overlap_and_period(tmp_path):
+    """tools/rt_pair_trace.py: on a synthetic trace where
+    each fold's traced start lies 3 us before its round trip's end, it reports
+    the overlap, the fold's tail behind the round trip and the pair period."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(TOOLS), "..", "tools"))
+    import rt_pair_trace as rp
+    csv_path = tmp_path / "kernel_trace.csv"
+    rows = ["Kind,Dispatch_Id,Queue_Id,Kernel_Name,Grid_Size_X,Start_Timestamp,End_Timestamp"]
+    t = 1_000_000
+    for i in range(4):
+        rows.append(f"KERNEL_DISPATCH,{2 * i},1,\"void hpdct::roundtrip_duo_kernel<true, 2>(...)\",2097152,{t},{t + 73000}")
+        rows.append(f"KERNEL_DISPATCH,{2 * i + 1},1,\"void hpdct::rt_spread_finish_kernel<64>(...)\",64,"
+                    f"{t + 70000},{t + 74900}")
+        t += 75000
+    csv_path.write_text("\n".join(rows) + "\n")
+    ps = rp.pairs(rp.load(str(csv_path)), 2097152)
+    assert len(ps) == 4
+    assert all(abs(p["gap"] + 3.0) < 1e-9 and abs(p["tail"] - 1.9) < 1e-9 and abs(p["fin"] - 4.9) < 1e-9
+               for p in ps)
+    assert [p["period"] for p in ps] == [75.0, 75.0, 75.0, None]

@@ -73,7 +73,10 @@ for s in "$@"; do
             -d "$OUT/prof_bench" -o hpdct -- "${bench_cmd[@]/#bench.py/$ROOT/bench.py}") || exit $?
         python3 tools/trace_summary.py "$(ls "$OUT"/prof_bench/*/hpdct_kernel_trace.csv \
             "$OUT"/prof_bench/hpdct_kernel_trace.csv 2>/dev/null | head -n1)" \
-            --bench "$OUT/rocprof_bench.log" --warmup 5 --steps 20 --out "$OUT/trace_summary.md" > /dev/null || true ;;
+            --bench "$OUT/rocprof_bench.log" --warmup 5 --steps 20 --out "$OUT/trace_summary.md" > /dev/null || true
+        python3 tools/rt_pair_trace.py "$(ls "$OUT"/prof_bench/*/hpdct_kernel_trace.csv \
+            "$OUT"/prof_bench/hpdct_kernel_trace.csv 2>/dev/null | head -n1)" --grid 2097152 \
+            --out "$OUT/rt_pairs.md" > /dev/null || true ;;
     shard)
         step shard_f32 120 cuda-dct-idct_amd/bin/benchmark_hpdct 16384 5 --gpus 1 || exit $?
         step shard_i8 120 cuda-dct-idct_amd/bin/benchmark_hpdct 16384 5 --gpus 1 --int8 || exit $? ;;

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Start/end stamps of consecutive (round trip, sums fold) pairs in a
+rocprofv3 --kernel-trace CSV: does the traced duration of
+the one-wave rt_spread_finish_kernel overlap the round trip before it, and
+what does one pair cost from one round trip's start to the next's?
+
+  python tools/rt_pair_trace.py <kernel_trace.csv> [--grid N] [--out pairs.md]
+
+A pair is a roundtrip_duo_kernel dispatch followed, on the same queue, by an
+rt_spread_finish_kernel dispatch.  Per pair (times in us):
+  rt        round trip end - start
+  fin       fold end - start
+  gap       fold start - round-trip end (negative: the fold's traced start
+            lies before the round trip has ended)
+  tail      fold end - round-trip end (what the fold adds behind the round trip)
+  period    next pair's round-trip start - this round-trip start, when the
+            next dispatch on the queue is that next round trip (back to back)
+Development tool; reads a trace, runs nothing.
+"""
+import argparse
+import csv
+import statistics
+import sys
+
+
+def load(path):
+    rows = []
+    with open(path, newline="") as fh:
+        for r in csv.DictReader(fh):
+            if r.get("Kind", "KERNEL_DISPATCH") != "KERNEL_DISPATCH":
+                continue
+            rows.append({"id": int(r["Dispatch_Id"]), "queue": r.get("Queue_Id", "0"), "name": r["Kernel_Name"],
+                         "grid": int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1),
+                         "t0": int(r["Start_Timestamp"]), "t1": int(r["End_Timestamp"])})
+    rows.sort(key=lambda r: r["id"])
+    return rows
+
+
+def pairs(rows, grid=None):
+    by_q = {}
+    for r in rows:
+        by_q.setdefault(r["queue"], []).append(r)
+    out = []
+    for q in by_q.values():
+        for i in range(len(q) - 1):
+            a, b = q[i], q[i + 1]
+            if "roundtrip_duo_kernel" not in a["name"] or "rt_spread_finish_kernel" not in b["name"]:
+                continue
+            if grid is not None and a["grid"] != grid:
+                continue
+            nxt = q[i + 2] if i + 2 < len(q) else None
+            period = None
+            if nxt is not None and "roundtrip_duo_kernel" in nxt["name"] and nxt["grid"] == a["grid"]:
+                period = (nxt["t0"] - a["t0"]) / 1e3
+            out.append({"name": a["name"][:60], "grid": a["grid"], "rt": (a["t1"] - a["t0"]) / 1e3,
+                        "fin": (b["t1"] - b["t0"]) / 1e3, "gap": (b["t0"] - a["t1"]) / 1e3,
+                        "tail": (b["t1"] - a["t1"]) / 1e3, "period": period})
+    return out
+
+
+def summary(vals):
+    vals = [v for v in vals if v is not None]
+    if not vals:
+        return "-"
+    return (f"{statistics.fmean(vals):.2f} / {statistics.median(vals):.2f} / {min(vals):.2f} / {max(vals):.2f}"
+            f" (n={len(vals)})")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--grid", type=int, default=None, help="only round trips of this grid size (threads)")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    ps = pairs(load(a.trace), a.grid)
+    if not ps:
+        print("no (roundtrip_duo_kernel, rt_spread_finish_kernel) pairs found", file=sys.stderr)
+        return 1
+    lines = ["| per pair, us | mean / median / min / max |", "|---|---|"]
+    for k, label in (("rt", "round trip (end - start)"), ("fin", "fold (end - start)"),
+                     ("gap", "fold start - round-trip end"), ("tail", "fold end - round-trip end"),
+                     ("period", "round-trip start to next round-trip start (back to back)")):
+        lines.append(f"| {label} | {summary([p[k] for p in ps])} |")
+    overlap = sum(1 for p in ps if p["gap"] < 0)
+    lines.append("")
+    lines.append(f"{len(ps)} pairs ({ps[0]['name']}, grid {ps[0]['grid']}); fold's traced start before the round "
+                 f"trip's end in {overlap} of them.")
+    bb = [p for p in ps if p["period"] is not None]
+    if bb:
+        lines.append(f"Back-to-back pairs: mean period {statistics.fmean(p['period'] for p in bb):.2f} us against "
+                     f"mean rt + fin {statistics.fmean(p['rt'] + p['fin'] for p in bb):.2f} us and mean "
+                     f"rt + tail {statistics.fmean(p['rt'] + p['tail'] for p in bb):.2f} us.")
+    text = "\n".join(lines) + "\n"
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(text)
+    print(text)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
