@@ -306,16 +306,22 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
 // split at 2^22, rt_sse_split): 1,096 VALU per wave instead of 1,163 and
 // 73.7-74.0 us against 74.5-75.2 (profiles/r05/f/).
 
-// kSets: 32-tile runs per wave, the wave's runs a grid apart (the sums of all
-// of them leave in one epilogue); kSpreadN: sub-slots of the spread slot.
-// Two more kSpreadN values exist for tools/kb_rt's decomposition of the sums'
-// cost only: 0 writes one plain 32-B record per wave (no atomics), < 0
-// computes the sums and skips the atomics when sums is null.
-template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSets = 1,
-          int kSpreadN = kRtSpread>
-__global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void roundtrip_duo_kernel(
-    const uint8_t* __restrict__ img, float* __restrict__ coef, void* __restrict__ recon, RtSums* __restrict__ sums,
-    TileGrid g, QParams qp) {
+// The sums of one wave after its runs: four 32-bit DPP sums (each add takes
+// its DPP operand directly; every one stays below 2^32 over a wave: 32 pixels
+// per lane and run, kSets <= 8), wave-uniform; sse_f32 rebuilt as 64 bits.
+struct DuoWaveSums {
+    unsigned long long fs;  // sse_f32 in fixed point (2^-16)
+    uint32_t se, sx;        // sse_u8, sum_x2
+    bool bad;               // some chain was non-finite or too large (kRtSseF32Invalid)
+};
+
+// The body both round-trip kernels share: the Q tables to LDS, the wave's
+// kSets runs of 32 tiles (a grid apart), and the wave's sums (kStats).
+// kSets: 32-tile runs per wave.
+template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT, int kSets>
+__device__ __forceinline__ DuoWaveSums rt_duo_waves(const uint8_t* __restrict__ img, float* __restrict__ coef,
+                                                    void* __restrict__ recon, const TileGrid& g, const QParams& qp,
+                                                    uint32_t& wave_out) {
     static_assert(kQMode == 1 || kQMode == 2, "duo round trip: verified quotient only");
     constexpr uint32_t kW = kBlockT / 64u;
 
@@ -328,6 +334,7 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
     const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, h = lane >> 5;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kW + wv);
+    wave_out = wave;
     uint32_t f_hi = 0u, f_lo = 0u;  // this lane's sse_f32 chains in fixed point over its runs, split at 2^22
     bool ok = true;
     uint32_t acc_xx = 0u, acc_xr = 0u, acc_rr = 0u;
@@ -353,32 +360,46 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
         }
     });
 
+    DuoWaveSums out{0ull, 0u, 0u, false};
     if constexpr (kStats) {
-        // the wave's sums: four 32-bit DPP sums (each add takes its DPP
-        // operand directly; every one stays below 2^32 over a wave: 32 pixels
-        // per lane and run, kSets <= 8), sse_f32 rebuilt as 64 bits in scalar
-        // registers; lane 0 adds into sub-slot (wave % kSpreadN) of the
-        // spread slot: no LDS, no barrier.  Its atomics take a per-lane zero
-        // offset, so they stay single atomics (no uniform-address rewrite).
         static_assert(kSets <= 8, "32-bit wave sums");
         const uint32_t e8 = acc_xx + acc_rr - 2u * acc_xr;
         const uint32_t sh = wave_sum_dpp(f_hi), sl = wave_sum_dpp(f_lo);
-        const uint32_t sx = wave_sum_dpp(acc_xx), se = wave_sum_dpp(e8);
-        const unsigned long long fs = (static_cast<unsigned long long>(sh) << 22) + sl;
-        const bool bad = __builtin_amdgcn_ballot_w64(!ok) != 0;
-        if (lane == 0u && (kSpreadN > 0 || sums)) {
+        out.sx = wave_sum_dpp(acc_xx), out.se = wave_sum_dpp(e8);
+        out.fs = (static_cast<unsigned long long>(sh) << 22) + sl;
+        out.bad = __builtin_amdgcn_ballot_w64(!ok) != 0;
+    }
+    return out;
+}
+
+// kSpreadN: sub-slots of the spread slot.  Two more kSpreadN values exist for
+// tools/kb_rt's decomposition of the sums' cost only: 0 writes one plain 32-B
+// record per wave (no atomics), < 0 computes the sums and skips the atomics
+// when sums is null.
+template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT = 256, int kWaves = 6, int kSets = 1,
+          int kSpreadN = kRtSpread>
+__global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void roundtrip_duo_kernel(
+    const uint8_t* __restrict__ img, float* __restrict__ coef, void* __restrict__ recon, RtSums* __restrict__ sums,
+    TileGrid g, QParams qp) {
+    uint32_t wave;
+    const DuoWaveSums w = rt_duo_waves<kStats, kQMode, kRecon, kRun, kBlockT, kSets>(img, coef, recon, g, qp, wave);
+    if constexpr (kStats) {
+        // lane 0 adds into sub-slot (wave % kSpreadN) of the spread slot: no
+        // LDS, no barrier.  Its atomics take a per-lane zero offset, so they
+        // stay single atomics (no uniform-address rewrite).
+        if ((threadIdx.x & 63u) == 0u && (kSpreadN > 0 || sums)) {
             uint32_t z = 0u;
             asm volatile("" : "+v"(z));
             if constexpr (kSpreadN == 0) {
                 auto* const dst = reinterpret_cast<unsigned long long*>(sums) + wave * 4u + z;
-                dst[0] = bad ? (fs | kRtSseF32Invalid) : fs, dst[1] = se, dst[2] = sx;
+                dst[0] = w.bad ? (w.fs | kRtSseF32Invalid) : w.fs, dst[1] = w.se, dst[2] = w.sx;
             } else {
                 constexpr uint32_t kN = kSpreadN < 0 ? -kSpreadN : kSpreadN;
                 auto* const dst = reinterpret_cast<unsigned long long*>(sums) + (wave % kN) * kRtSpreadStride + z;
-                if (fs) atomicAdd(dst, fs);
-                if (bad) atomicOr(dst, kRtSseF32Invalid);
-                if (se) atomicAdd(dst + 1, static_cast<unsigned long long>(se));
-                if (sx) atomicAdd(dst + 2, static_cast<unsigned long long>(sx));
+                if (w.fs) atomicAdd(dst, w.fs);
+                if (w.bad) atomicOr(dst, kRtSseF32Invalid);
+                if (w.se) atomicAdd(dst + 1, static_cast<unsigned long long>(w.se));
+                if (w.sx) atomicAdd(dst + 2, static_cast<unsigned long long>(w.sx));
             }
         }
     }

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "kbench_rtduo_pk.hpp"
+#include "kbench_rtfold.hpp"
 
 using namespace hpdct;
 
@@ -112,6 +113,14 @@ void duo_dec(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipS
     }
 }
 
+// round 6: the fold inside the round-trip kernel (tickets, the last wave
+// folds; roundtrip_duo_fold_kernel): one dispatch per launch
+template <int kMode>
+void duo_kfold(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((roundtrip_duo_fold_kernel<true, 2, kRtReconU8, 256, 6>), roundtrip_duo_grid(c.g, 256),
+                       dim3(256), 0, s, img, coef, recon, g_spread, c.sums, c.g, c.qp, kMode);
+}
+
 // the tile kernel with the product's sums path (spread sub-slot 0 + finish)
 template <bool kStats>
 void tile_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
@@ -201,6 +210,12 @@ int main(int argc, char** argv) {
         {"occ", "duo no sums, w7", duo_sp<false, 256, 7>, false},
         {"occ", "duo no sums, w8", duo_sp<false, 256, 8>, false},
         {"occ", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"fold", "duo + sums (product: kernel + fold kernel)", duo_sp<true, 256, 6>, true},
+        {"fold", "duo + sums, fold in the kernel (tickets)", duo_kfold<0>, true},
+        {"fold", "duo + sums, no finish kernel (timing)", duo_fin<1>, false},
+        {"fold", "duo no sums", duo_sp<false, 256, 6>, false},
+        {"fold", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"fold", "duo + sums, fold in the kernel again", duo_kfold<0>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},

@@ -4,7 +4,7 @@ rocprofv3 --kernel-trace CSV: does the traced duration of
 the one-wave rt_spread_finish_kernel overlap the round trip before it, and
 what does one pair cost from one round trip's start to the next's?
 
-  python tools/rt_pair_trace.py <kernel_trace.csv> [--grid N] [--out pairs.md]
+  python tools/rt_pair_trace.py <kernel_trace.csv> [--grid N] [--name SUBSTR] [--last K] [--out pairs.md]
 
 A pair is a roundtrip_duo_kernel dispatch followed, on the same queue, by an
 rt_spread_finish_kernel dispatch.  Per pair (times in us):
@@ -36,7 +36,7 @@ def load(path):
     return rows
 
 
-def pairs(rows, grid=None):
+def pairs(rows, grid=None, name=None):
     by_q = {}
     for r in rows:
         by_q.setdefault(r["queue"], []).append(r)
@@ -48,9 +48,11 @@ def pairs(rows, grid=None):
                 continue
             if grid is not None and a["grid"] != grid:
                 continue
+            if name is not None and name not in a["name"]:
+                continue
             nxt = q[i + 2] if i + 2 < len(q) else None
             period = None
-            if nxt is not None and "roundtrip_duo_kernel" in nxt["name"] and nxt["grid"] == a["grid"]:
+            if nxt is not None and nxt["name"] == a["name"] and nxt["grid"] == a["grid"]:
                 period = (nxt["t0"] - a["t0"]) / 1e3
             out.append({"name": a["name"][:60], "grid": a["grid"], "rt": (a["t1"] - a["t0"]) / 1e3,
                         "fin": (b["t1"] - b["t0"]) / 1e3, "gap": (b["t0"] - a["t1"]) / 1e3,
@@ -70,9 +72,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--grid", type=int, default=None, help="only round trips of this grid size (threads)")
+    ap.add_argument("--name", default=None, help="only round trips whose kernel name contains this")
+    ap.add_argument("--last", type=int, default=0, help="only the last K pairs (a bench leg's timed launches)")
     ap.add_argument("--out")
     a = ap.parse_args()
-    ps = pairs(load(a.trace), a.grid)
+    ps = pairs(load(a.trace), a.grid, a.name)
+    if a.last:
+        ps = ps[-a.last:]
     if not ps:
         print("no (roundtrip_duo_kernel, rt_spread_finish_kernel) pairs found", file=sys.stderr)
         return 1
