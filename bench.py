@@ -390,6 +390,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = _cpu_baseline(n)
 
+    if "extras" in result:
+        # last in the line, so a record that keeps only the line's tail still
+        # holds every kernel against its ceiling
+        result["kernel_status"] = kernel_status(result)
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if use_pg:
@@ -398,6 +402,44 @@ def main():
         except Exception:
             pass
     return 0
+
+
+def kernel_status(result):
+    """{kernel: [us, ceiling_us, frac_of_ceiling, status]} for every timed
+    kernel of the line that has a reachable ceiling: the
+    copy of the same bytes (hpdct_copy_ceiling) for the HBM kernels, the
+    same-bytes copy on the forward's own grid for C2 (cache-resident), the
+    copy-only PCIe pipeline for C5 (frames/s, higher is better; frac = rate /
+    ceiling).  status: "done" at >= DONE_FRAC of the ceiling, else "open"."""
+    ex = result.get("extras", {})
+    out = {}
+
+    def put(name, us, ceil_us):
+        if us and ceil_us:
+            f = round(ceil_us / us, 3)
+            out[name] = [round(us, 2), round(ceil_us, 2), f, "done" if f >= DONE_FRAC else "open"]
+
+    rf = result.get("roofline", {})
+    put("headline_fwd_u8_f32", rf.get("kernel_us_avg"), rf.get("copy_ceiling_us"))
+    for key in ("fwd_u8_i8", "inv_f32_f32", "fwd_f32_f32_runtimeT"):
+        if key in ex:
+            put(key, ex[key].get("kernel_us_avg"), ex[key].get("ceiling_us"))
+    for key, line in ex.get("dropin", {}).items():
+        put("dropin." + key.split(" ")[0] + ("_cublasv2" if "cublas" in key else ""), line.get("kernel_us_avg"),
+            line.get("ceiling_us"))
+    c3 = ex.get("c3_roundtrip", {})
+    for key in ("one_pass", "one_pass_f32_recon", "one_pass_sums_ring"):
+        if key in c3:
+            put("c3." + key, c3[key].get("kernel_us_avg"), c3[key].get("ceiling_us"))
+    fl = ex.get("c2_fwd_u8_f32", {}).get("floor", {})
+    put("c2_fwd_u8_f32", fl.get("forward_us"), fl.get("copy_same_bytes_us"))
+    for k in ("f32", "i8"):
+        c5 = ex.get("c5", {}).get(k)
+        if c5 and c5.get("copy_only_ceiling_frames_per_s"):
+            f = round(c5["frames_per_s_total"] / c5["copy_only_ceiling_frames_per_s"], 3)
+            out["c5_" + k + "_frames_per_s"] = [c5["frames_per_s_total"], c5["copy_only_ceiling_frames_per_s"], f,
+                                               "done" if f >= DONE_FRAC else "open"]
+    return out
 
 
 def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_over_ranks, timed_loop0, imgs, outs, px,
@@ -425,49 +467,45 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         return timed_loop0(calls, steps, 0)
 
     steps = EXTRA_STEPS
-    ceilings = {}
+    ceil_jobs = []
 
-    scratch = {}
+    def ceiling_later(line, srcs, o0s, o1s=None):
+        """Queue the copy ceiling of the kernel `line` describes (VERDICT r5
+        item 2): hpdct_copy_ceiling moving the kernel's own bytes per pixel
+        over the kernel's OWN rotating planes (its inputs, its outputs, its
+        write-back plane; the two-output patterns vary by ~10 % with where the
+        planes sit, so the ceiling must share the kernel's), timed like the
+        kernel at each residency cap of CEIL_CAPS, the fastest kept.  The
+        copies overwrite those outputs, so they run after every leg that
+        reads them (run_ceilings)."""
+        ceil_jobs.append((line, srcs, o0s, o1s))
 
-    def planes(dtype, which):
-        """two scratch output planes per (dtype, output slot): the ceilings
-        never write over a kernel's inputs or outputs"""
-        if (dtype, which) not in scratch:
-            scratch[(dtype, which)] = [torch.empty((n, n), dtype=dtype, device=dev) for _ in range(2)]
-        return scratch[(dtype, which)]
-
-    def ceiling(srcs, o0_dtype, o1_dtype=None):
-        """The copy ceiling of a kernel: hpdct_copy_ceiling
-        moving the kernel's own bytes per pixel, reading the kernel's rotating
-        inputs and writing two scratch planes per output (as the inverse and
-        round-trip legs write two), timed like the kernel at each residency cap
-        of CEIL_CAPS; the fastest is the ceiling.  One measurement per byte
-        pattern (in, out0, out1 bytes), shared by the kernels that move it."""
+    def measure_ceiling(srcs, o0s, o1s):
+        by = {}
+        for cap in CEIL_CAPS:
+            calls = [hpdct.bind_copy_ceiling(srcs[i], o0s[i % len(o0s)], o1s[i % len(o1s)] if o1s else None,
+                                             cap_waves=cap, stream=stream) for i in range(len(srcs))]
+            rms, _, _ = timed_loop(calls, steps, 5)
+            by[str(cap)] = round(rms / steps * 1e3, 2)
+        best = min(by, key=by.get)
         size = {torch.uint8: 1, torch.int8: 1, torch.float32: 4}
-        key = (size[srcs[0].dtype], size[o0_dtype], size[o1_dtype] if o1_dtype else 0)
-        if key not in ceilings:
-            o0s = planes(o0_dtype, 0)
-            o1s = planes(o1_dtype, 1) if o1_dtype else None
-            by = {}
-            for cap in CEIL_CAPS:
-                calls = [hpdct.bind_copy_ceiling(srcs[i], o0s[i % 2], o1s[i % 2] if o1s else None,
-                                                 cap_waves=cap, stream=stream) for i in range(len(srcs))]
-                rms, _, _ = timed_loop(calls, steps, 5)
-                by[str(cap)] = round(rms / steps * 1e3, 2)
-            best = min(by, key=by.get)
-            ceilings[key] = {"us": by[best], "cap_waves": int(best), "by_cap_us": by,
-                             "bytes_per_px": sum(key), "pattern": f"{key[0]} B in, {key[1]}"
-                                                                  + (f" + {key[2]}" if key[2] else "") + " B out"}
-        return ceilings[key]
+        key = (size[srcs[0].dtype], size[o0s[0].dtype], size[o1s[0].dtype] if o1s else 0)
+        return {"us": by[best], "cap_waves": int(best), "by_cap_us": by, "bytes_per_px": sum(key),
+                "pattern": f"{key[0]} B in, {key[1]}" + (f" + {key[2]}" if key[2] else "") + " B out"}
 
-    def with_ceiling(line, ceil):
-        """ceiling_us / frac_of_ceiling beside hbm_frac, and the kernel's status:
-        done at >= DONE_FRAC of the copy of its own bytes"""
-        line["ceiling_us"] = ceil["us"]
-        line["frac_of_ceiling"] = round(ceil["us"] / line["kernel_us_avg"], 4)
-        line["ceiling"] = ceil
-        line["status"] = "done" if line["frac_of_ceiling"] >= DONE_FRAC else "open"
-        return line
+    def run_ceilings():
+        """ceiling_us / frac_of_ceiling beside hbm_frac, and each kernel's
+        status: done at >= DONE_FRAC of the copy of its own bytes"""
+        for line, srcs, o0s, o1s in ceil_jobs:
+            ceil = measure_ceiling(srcs, o0s, o1s)
+            if "kernel_us_avg" not in line:  # the headline's own entry
+                line.update(ceil)
+                continue
+            line["ceiling_us"] = ceil["us"]
+            line["frac_of_ceiling"] = round(ceil["us"] / line["kernel_us_avg"], 4)
+            line["ceiling"] = ceil
+            line["status"] = "done" if line["frac_of_ceiling"] >= DONE_FRAC else "open"
+        ceil_jobs.clear()
 
     if True:
         # fp32 in -> fp32 out (the reference's own data types; compat kernel)
@@ -476,24 +514,25 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         T = torch.from_numpy(hpdct.default_transform()).to(dev)
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, stream=stream) for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_f32_f32_runtimeT"] = with_ceiling(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world, "fdct_f32_f32_duo_runtimeT", n),
-            ceiling(f32_in, torch.float32))
+        extras["fwd_f32_f32_runtimeT"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["f32_f32"], world,
+                                               "fdct_f32_f32_duo_runtimeT", n)
+        ceiling_later(extras["fwd_f32_f32_runtimeT"], f32_in, f32_out)
         # the headline's own copy ceiling (1 B in, 4 B out), beside its roofline
-        extras["headline_ceiling"] = ceiling(imgs, torch.float32)
+        extras["headline_ceiling"] = {}
+        ceiling_later(extras["headline_ceiling"], imgs, outs)
         # u8 -> int8 wire format
         i8 = [torch.empty((n, n), dtype=torch.int8, device=dev) for _ in range(args.sets)]
         calls = [hpdct.bind("fwd", imgs[s], i8[s], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["fwd_u8_i8"] = with_ceiling(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world, "fdct_u8_i8", n), ceiling(imgs, torch.int8))
+        extras["fwd_u8_i8"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["u8_i8"], world, "fdct_u8_i8", n)
+        ceiling_later(extras["fwd_u8_i8"], imgs, i8)
         # inverse fp32 -> fp32 (idct_all_blocks_cuda's data path)
         rec = [torch.empty((n, n), dtype=torch.float32, device=dev) for _ in range(2)]
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
-        extras["inv_f32_f32"] = with_ceiling(
-            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world, "idct_f32_f32_duo", n),
-            ceiling(outs, torch.float32))
+        extras["inv_f32_f32"] = _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["inv_f32_f32"], world,
+                                      "idct_f32_f32_duo", n)
+        ceiling_later(extras["inv_f32_f32"], outs, rec)
         # the drop-in surface: exactly what the compat entry points launch
         # (hpdct_compat.cpp), i.e. what a caller of the reference's functions
         # gets: fp32 planes, the caller's T, and the reference's in-place side
@@ -506,33 +545,36 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                  for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["dct_all_blocks_cuda"] = dict(
-            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world,
-                               "compat_fwd_f32_wb", n), ceiling(f32_in, torch.float32, torch.float32)),
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_f32_wb", n),
             launches="fdct_duo_kernel<quant, runtime T, writeback>",
             bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["idct_all_blocks_cuda"] = dict(
-            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv"], world, "compat_inv_f32",
-                               n), ceiling(outs, torch.float32)),
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv"], world, "compat_inv_f32", n),
             launches="idct_duo_kernel<dequant, runtime T>", bytes_note="4 B read + 4 B written")
         calls = [hpdct.bind("fwd", f32_in[i], f32_out[i], transform=T, writeback_shift=True, row_first=True,
                             stream=stream) for i in range(len(f32_in))]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["dct_all_blocks (cublasDCTv2)"] = dict(
-            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world,
-                               "compat_fwd_rowfirst_wb", n), ceiling(f32_in, torch.float32, torch.float32)),
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_fwd"], world, "compat_fwd_rowfirst_wb", n),
             launches="rowfirst_duo_kernel<forward, quant, runtime T, writeback>",
             bytes_note="4 B read + 4 B coefficients + 4 B X-128 written back")
         calls = [hpdct.bind("inv", outs[s], rec[s % 2], transform=T, row_first=True, writeback_dequant=True,
                             stream=stream) for s in range(args.sets)]
         rms, k, _ = timed_loop(calls, steps, 5)
         dropin["idct_all_blocks (cublasDCTv2)"] = dict(
-            with_ceiling(_line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv_wb"], world,
-                               "compat_inv_rowfirst_wb", n), ceiling(outs, torch.float32, torch.float32)),
+            _line(px, rms / steps, float(k.mean()), BYTES_PER_PX["compat_inv_wb"], world, "compat_inv_rowfirst_wb",
+                  n),
             launches="rowfirst_duo_kernel<inverse, dequant, runtime T, writeback>",
             bytes_note="4 B read + 4 B pixels + 4 B q*Q written back")
         extras["dropin"] = dropin
+        # the drop-in kernels' ceilings: their own planes, the write-back plane
+        # being the input (X-128) or the coefficient plane (q*Q) in place
+        ceiling_later(dropin["dct_all_blocks_cuda"], f32_in, f32_out, f32_in)
+        ceiling_later(dropin["idct_all_blocks_cuda"], outs, rec)
+        ceiling_later(dropin["dct_all_blocks (cublasDCTv2)"], f32_in, f32_out, f32_in)
+        ceiling_later(dropin["idct_all_blocks (cublasDCTv2)"], outs, rec, outs)
         # the write-backs above changed the fp32 inputs / coefficients: the
         # later extras recompute what they read
         # the reference's own two GPU decompositions of the same arithmetic, on
@@ -627,8 +669,6 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         qa = hpdct.quality_from_sums(hpdct.sums_from_buffer(ring[0]), px)
         k2 = np.array([acc_ms])
         rms2 = acc_ms * steps
-        c3_ceil_u8 = ceiling(imgs, torch.float32, torch.uint8)
-        c3_ceil_f32 = ceiling(imgs, torch.float32, torch.float32)
         # the device sums against torch's on the two-kernel output: the integer
         # fields exactly (double is exact below 2^53)
         sums_exact = sums_one["sse_u8"] == int(se8) and sums_one["sum_x2"] == int(sx)
@@ -637,26 +677,29 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
             "mse_u8": se8 / px, "peen_u8_pct": 100.0 * (se8 / sx) ** 0.5,
             "two_kernels": {"ms_per_frame": round(rt_ms, 5), "gpx_s": round(world * px / (rt_ms * 1e-3) / 1e9, 2),
                             "bytes_per_px": 10, "note": "forward u8->f32 then inverse f32->u8, PEEN/MSE by torch"},
-            "one_pass": dict(with_ceiling(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums",
-                                                n), c3_ceil_u8),
+            "one_pass": dict(_line(px, one_ms, float(k1.mean()), 6, world, "roundtrip_u8_f32_u8_sums", n),
                              quality_from_device_sums=qd, sums_exact_vs_two_kernels=sums_exact,
                              note="hpdct_roundtrip_u8: coefficients + u8 reconstruction + PEEN/MSE sums in one "
                                   "pass (the round trip + a one-wave kernel that moves the sums from the library's "
                                   "slot over the caller's struct); bit-identical to the two kernels"),
-            "one_pass_f32_recon": dict(with_ceiling(_line(px, f32_ms, float(kf.mean()), 9, world), c3_ceil_f32),
+            "one_pass_f32_recon": dict(_line(px, f32_ms, float(kf.mean()), 9, world),
                                        recon_equals_two_kernels=f32_recon_exact, sums_equal_u8_pass=f32_sums_equal,
                                        note="hpdct_roundtrip_u8 with HPDCT_F32: coefficients + fp32 R+128 (the "
                                             "reference's float output) + PEEN/MSE sums in one pass"),
-            "one_pass_sums_ring": dict(with_ceiling(_line(px, acc_ms, float(k2.mean()), 6, world), c3_ceil_u8),
-                                       quality_from_device_sums=qa,
+            "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
                                        ring_sums_exact=ring_exact,
                                        note="hpdct_roundtrip_u8_accumulate, one slot per timed launch of a fresh "
                                             "caller-zeroed ring (its memset outside the timed region); the warm-up "
                                             "accumulates into a ring of its own; ring_sums_exact: every slot equals "
                                             "its frame's hpdct_roundtrip_u8 sums"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
+        c3 = extras["c3_roundtrip"]
+        ceiling_later(c3["one_pass"], imgs, outs, rt_px)
+        ceiling_later(c3["one_pass_f32_recon"], imgs, outs, rec)
+        ceiling_later(c3["one_pass_sums_ring"], imgs, outs, rt_px)
+        # every leg that reads these planes has run: the copies may overwrite them
+        run_ceilings()
         del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc, warm, warm_ring, ref_sums, want
-        scratch.clear()
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024

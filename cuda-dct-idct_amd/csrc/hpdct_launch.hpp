@@ -221,9 +221,21 @@ size_t duo_cap_lds(K kern) {
 template <unsigned kV, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t fdct_duo_go(const float* img, float* out, float* shifted, const TileGrid& g, const float* t_dev,
                        const QParams& q, float shift, hipStream_t s) {
-    // uncapped: the quantising fp32 forward (caller's T, full chains, IEEE
-    // division) is VALU-heavy, and the cap made it slower in the driver's bench
-    // (91.6 -> 101.8 us, drop-in with write-back 135.6 -> 135.1)
+    // The checked 3-op quotient (integer table: the JPEG default, the drop-in
+    // surface) takes the inverse's residency cap since round 6: 8192^2
+    // dct_all_blocks_cuda 125.7 against 131.5 us uncapped, without the
+    // write-back 88.1 against 89.5 (tools/kbench3 groups dropcap / fwdcap,
+    // profiles/r06/).  With IEEE division (any other table) it stays uncapped:
+    // VALU-heavier, the cap made it slower (round 3: 91.6 -> 101.8 us).
+    if constexpr ((kV & kVarFastDivChecked) != 0) {
+        if (DuoShape<kV>::capped(g)) {
+            constexpr unsigned kC = DuoShape<kV>::kCapped;
+            auto* kern = fdct_duo_kernel<kQuant, kBuiltinT, kWriteback, kC>;
+            hipLaunchKernelGGL(kern, duo_grid(g, kBlock<kC>), dim3(kBlock<kC>), duo_cap_lds(kern), s, img, out,
+                               shifted, g, t_dev, q, shift);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((fdct_duo_kernel<kQuant, kBuiltinT, kWriteback, kV>), duo_grid(g, kBlock<kV>), dim3(kBlock<kV>),
                        0, s, img, out, shifted, g, t_dev, q, shift);
     return hipGetLastError();

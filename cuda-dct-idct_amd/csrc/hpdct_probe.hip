@@ -52,9 +52,10 @@ __device__ __forceinline__ uint32_t pack4_trunc(const float4& f) {
     return (static_cast<uint32_t>(f.x) & 255u) | (static_cast<uint32_t>(f.y) & 255u) << 8 |
            (static_cast<uint32_t>(f.z) & 255u) << 16 | (static_cast<uint32_t>(f.w) & 255u) << 24;
 }
+// in and o1 may be one plane (an in-place write-back, as the drop-in
+// kernels' X-128 and q*Q planes): each lane stores only what it loaded.
 template <int kIn, int kO0, int kO1>
-__global__ __launch_bounds__(64) void copy_ceiling_kernel(const void* __restrict__ in, void* __restrict__ o0,
-                                                          void* __restrict__ o1) {
+__global__ __launch_bounds__(64) void copy_ceiling_kernel(const void* in, void* __restrict__ o0, void* o1) {
     constexpr bool kWide = kIn == 4 || kO0 == 4 || kO1 == 4;
     constexpr uint32_t kA = kWide ? 4u : 8u, kG = kCeilPx / (64u * kA);
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kCeilPx + threadIdx.x * kA;

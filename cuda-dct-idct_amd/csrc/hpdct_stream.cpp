@@ -203,7 +203,15 @@ hpdct_status run(hpdct_stream_ctx c, const uint8_t* const* h_frames, void* const
     for (int64_t f = 0; f < n_frames && e == hipSuccess; ++f) {
         const int s = static_cast<int>(f % nstreams);
         hipStream_t st = c->streams[s];
-        e = hipMemcpyAsync(c->in[s], h_frames[f], px, hipMemcpyHostToDevice, st);
+        // staggered start (round 6): stream s's first upload waits for stream
+        // s-1's, so the streams run out of phase and one stream's D2H copy
+        // overlaps the next one's H2D copy from the first frame on.  Started
+        // together they ran in step (all uploads, then all downloads) unless
+        // they happened to drift apart: int8 C5 0.70-0.91 of the copy-only
+        // duplex ceiling from box to box (BENCH_r05 extras.c5, profiles/r06/)
+        if (f > 0 && f < nstreams) e = hipStreamWaitEvent(st, c->done[s - 1], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(c->in[s], h_frames[f], px, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && f + 1 < nstreams && f + 1 < n_frames) e = hipEventRecord(c->done[s], st);
         if (e != hipSuccess) break;
         const hpdct_status hs =
             hpdct_forward(c->in[s], HPDCT_U8, c->out[s], c->out_type, height, width, nullptr, 0u, st);

@@ -53,8 +53,10 @@ hpdct_status hpdct_floor_probe(hpdct_probe_kind kind, const uint8_t* d_in, float
  * 8 pixels (8 B) when every plane is 1 B.  One-wave workgroups of 2,048
  * pixels each; cap_waves > 0 reserves LDS so that at most that many are
  * resident per CU (0: the hardware's limit).  n a positive multiple of 2048;
- * d_in and the outputs 16-byte aligned; async on `stream`.  bench.py times it
- * at a few caps and reports the fastest as the kernel's ceiling. */
+ * d_in and the outputs 16-byte aligned; d_out1 may be d_in (an in-place
+ * write-back, as the drop-in kernels' X-128 and q*Q planes); async on
+ * `stream`.  bench.py times it over each kernel's own planes at a few caps
+ * and reports the fastest as that kernel's ceiling. */
 hpdct_status hpdct_copy_ceiling(const void* d_in, hpdct_dtype in_type, void* d_out0, hpdct_dtype out0_type,
                                 void* d_out1, hpdct_dtype out1_type, int64_t n, int cap_waves, void* stream);
 

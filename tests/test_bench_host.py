@@ -164,3 +164,24 @@ def test_sustained_phase_default_on_and_switchable(monkeypatch):
     assert bench.parse().sustain_s > 0
     monkeypatch.setattr(sys, "argv", ["bench.py", "--sustain-s", "0"])
     assert bench.parse().sustain_s == 0
+
+
+def test_kernel_status_puts_every_kernel_beside_its_ceiling():
+    """the line ends with {kernel: [us, ceiling_us, frac,
+    status]}; "done" at >= DONE_FRAC of the copy of the kernel's own bytes,
+    C5 as frames/s against the copy-only pipeline."""
+    line = lambda us, ceil: {"kernel_us_avg": us, "ceiling_us": ceil}  # noqa: E731
+    res = {"roofline": {"kernel_us_avg": 56.0, "copy_ceiling_us": 54.0},
+           "extras": {"fwd_u8_i8": line(31.0, 22.0), "inv_f32_f32": line(86.0, 85.0),
+                      "dropin": {"dct_all_blocks_cuda": line(126.0, 122.0),
+                                 "idct_all_blocks (cublasDCTv2)": line(133.0, 122.0)},
+                      "c3_roundtrip": {"one_pass": line(75.0, 63.0)},
+                      "c2_fwd_u8_f32": {"floor": {"forward_us": 3.6, "copy_same_bytes_us": 3.3}},
+                      "c5": {"i8": {"frames_per_s_total": 2500.0, "copy_only_ceiling_frames_per_s": 2800.0}}}}
+    ks = bench.kernel_status(res)
+    assert ks["headline_fwd_u8_f32"] == [56.0, 54.0, round(54 / 56, 3), "done"]
+    assert ks["fwd_u8_i8"][3] == "open" and ks["inv_f32_f32"][3] == "done"
+    assert ks["dropin.dct_all_blocks_cuda"][3] == "done"
+    assert ks["dropin.idct_all_blocks_cublasv2"][2] == round(122 / 133, 3)
+    assert ks["c3.one_pass"][3] == "open" and ks["c2_fwd_u8_f32"][3] == "done"
+    assert ks["c5_i8_frames_per_s"] == [2500.0, 2800.0, round(2500 / 2800, 3), "open"]

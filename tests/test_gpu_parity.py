@@ -526,10 +526,22 @@ def test_capped_duo_writebacks_large_frame(hp, oracle, dev):
     16,400 waves of 32 tiles on 256 CUs) take the one-wave, residency-capped
     duo kernels (hpdct_launch.hpp DuoShape): the rows-first forward with the
     X-128 write-back, the rows-first inverse with the q*Q write-back and the
-    reference-order inverse with the q*Q write-back.  Ragged width (tiles_x =
-    1025).  Bit-exact, the write-back planes included."""
+    reference-order inverse with the q*Q write-back; since round 6 also the
+    reference-order forward (dct_all_blocks_cuda's kernel, checked quotient)
+    with the built-in and the caller's T, with and without its write-back.
+    Ragged width (tiles_x = 1025).  Bit-exact, the write-back planes included
+    (ADVICE r3)."""
     h, w = 4096, 8200
     img = oracle.hash_u8(h * w, seed=77).reshape(h, w).astype(np.float32)
+    ref = oracle.fdct(img)
+    T = to_dev(oracle.default_transform(), dev)
+    for transform in (None, T):
+        x = to_dev(img, dev)
+        got = hp.forward(x, transform=transform, writeback_shift=True)
+        assert bits_equal(to_host(got), ref), mismatches(to_host(got), ref)
+        assert bits_equal(to_host(x), img - np.float32(128))
+        got = hp.forward(to_dev(img, dev), transform=transform)
+        assert bits_equal(to_host(got), ref), mismatches(to_host(got), ref)
     x = to_dev(img, dev)
     q = hp.forward(x, row_first=True, writeback_shift=True)
     q_ref = oracle.fdct(img, row_first=True)

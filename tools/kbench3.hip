@@ -356,6 +356,20 @@ void dropin_fwd_cap(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        g_shift[set_of(in)], c.g, nullptr, c.qp, 128.0f);
 }
 
+// the drop-in forward as the compat entry points launch it (round 6 A/B): the
+// caller's T in a device buffer (bitwise the built-in one), the JPEG table's
+// checked quotient, uncapped (through round 5) or one-wave workgroups capped
+// per CU (round 6)
+float* g_T = nullptr;
+template <unsigned kVar, uint32_t kWg, bool kWb = true>
+void dropin_fwd_rt(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    auto* k = fdct_duo_kernel<true, false, kWb, kVar>;
+    static const size_t dyn = kWg ? cap_for(k, kWg) : 0;
+    float* src = g_coef[set_of(in)];
+    hipLaunchKernelGGL(k, duo_grid(c.g, kBlock<kVar>), dim3(kBlock<kVar>), dyn, s, src, static_cast<float*>(out),
+                       kWb ? g_shift[set_of(in)] : nullptr, c.g, g_T, c.qp, 128.0f);
+}
+
 int main(int argc, char** argv) {
     int n = 8192, hgt = 8192;
     if (argc > 1) {
@@ -554,6 +568,14 @@ int main(int argc, char** argv) {
         {"dropin", "dropin fwd f32 duo b64 cap 10 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 10>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo b64 cap 12 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 12>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo library again", dropin_fwd_cap<kDuoVar, 0>, 12, 4, true},
+        {"dropcap", "dropin uncapped (round 5)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0>, 12, 4, true},
+        {"dropcap", "dropin b64 cap 10", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10>, 12, 4, true},
+        {"dropcap", "dropin b64 cap 8", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 8>, 12, 4, true},
+        {"dropcap", "dropin b64 cap 10 again", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10>, 12, 4, true},
+        {"dropcap", "dropin uncapped again", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0>, 12, 4, true},
+        {"fwdcap", "fwd no wb uncapped (round 5)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0, false>, 8, 4, true},
+        {"fwdcap", "fwd no wb b64 cap 10", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10, false>, 8, 4, true},
+        {"fwdcap", "fwd no wb uncapped again", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0, false>, 8, 4, true},
         // round 4: the default JPEG table's per-position 3-op quantiser forms (kVarJpegQ) against the
         // verified 6-op form, in the product's dispatch, and the headline cap re-swept with them
         {"jq", "fwd u8->f32 library cap 10 (6-op)", prod_f32_fwd_cap<PK1, 10>, 5, 4, true},
@@ -693,16 +715,21 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc" ||
+               v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc" ||
                v.group == "rtring";
     });
     if (want_coef) {
         g_img = img;
         g_coef.resize(nsets);
         for (auto& p : g_coef) CK(hipMalloc(&p, px * 4));
-        if (std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "dropin"; })) {
+        if (std::any_of(vars.begin(), vars.end(),
+                        [](const Variant& v) {
+                            return v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap";
+                        })) {
             g_shift.resize(nsets);
             for (auto& p : g_shift) CK(hipMalloc(&p, px * 4));
+            CK(hipMalloc(&g_T, 64 * sizeof(float)));
+            CK(hipMemcpy(g_T, kBuiltinT.v, 64 * sizeof(float), hipMemcpyHostToDevice));
         }
         CK(hipMalloc(&g_sums, sizeof(RtSums)));
         CK(hipMalloc(&g_sums_ring, kRing * sizeof(RtSums)));
