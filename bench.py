@@ -634,27 +634,29 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         del onef, sums_f, r_ref
         # the same with a caller-zeroed ring of per-frame sums slots
         # (hpdct_roundtrip_u8_accumulate: the frame's sums are added to its
-        # slot by the same finish kernel).  The warm-up accumulates into a ring of its own; the
-        # timed launches go to a fresh zeroed ring, one slot each, so after the
-        # region every slot must hold exactly its frame's sums (ring_sums_exact)
+        # slot by the same finish kernel).  The warm-up runs the timed launches
+        # themselves into the ring (so every ring entry has its library slot, as
+        # in a pipeline that reuses its ring: a first use allocates), then the
+        # ring is zeroed outside the timed region and the timed launches go one
+        # per entry, so after the region every entry must hold exactly its
+        # frame's sums (ring_sums_exact)
         ref_sums = []
         for s in range(args.sets):
             b = torch.zeros(3, dtype=torch.int64, device=dev)
             hpdct.bind_roundtrip(imgs[s], outs[s], rt_px[0], b, stream=stream)()
             ref_sums.append(b)
-        warm_ring = torch.zeros((args.sets, 3), dtype=torch.int64, device=dev)
-        warm = [hpdct.bind_roundtrip(imgs[s], outs[s], rt_px[s % 2], warm_ring[s], stream=stream, accumulate=True)
-                for s in range(args.sets)]
         ring_n = steps
         ring = torch.zeros((ring_n, 3), dtype=torch.int64, device=dev)
         acc = [hpdct.bind_roundtrip(imgs[i % args.sets], outs[i % args.sets], rt_px[i % 2], ring[i], stream=stream,
                                     accumulate=True) for i in range(ring_n)]
         i, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < EXTRA_WARM_S or i < 2 * len(warm):
-            warm[i % len(warm)]()
+        while time.perf_counter() - t0 < EXTRA_WARM_S or i < 2 * len(acc):
+            acc[i % len(acc)]()
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        ring.zero_()
         torch.cuda.synchronize()
         barrier()
         ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -688,10 +690,10 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
                                             "reference's float output) + PEEN/MSE sums in one pass"),
             "one_pass_sums_ring": dict(_line(px, acc_ms, float(k2.mean()), 6, world), quality_from_device_sums=qa,
                                        ring_sums_exact=ring_exact,
-                                       note="hpdct_roundtrip_u8_accumulate, one slot per timed launch of a fresh "
-                                            "caller-zeroed ring (its memset outside the timed region); the warm-up "
-                                            "accumulates into a ring of its own; ring_sums_exact: every slot equals "
-                                            "its frame's hpdct_roundtrip_u8 sums"),
+                                       note="hpdct_roundtrip_u8_accumulate, one ring entry per timed launch; the "
+                                            "warm-up runs the same launches into the ring, which is then zeroed "
+                                            "outside the timed region; ring_sums_exact: every entry equals its "
+                                            "frame's hpdct_roundtrip_u8 sums"),
             "note": "uniform-noise frame: not comparable with README's 'Circuit' image (4.66 %)"}
         c3 = extras["c3_roundtrip"]
         ceiling_later(c3["one_pass"], imgs, outs, rt_px)
@@ -699,7 +701,7 @@ def _extras(args, hpdct, torch, dist, dev, world, rank, stream, barrier, max_ove
         ceiling_later(c3["one_pass_sums_ring"], imgs, outs, rt_px)
         # every leg that reads these planes has run: the copies may overwrite them
         run_ceilings()
-        del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc, warm, warm_ring, ref_sums, want
+        del f32_in, i8, rec, r8, x, rt_px, sums_buf, ring, acc, ref_sums, want
         # C2: 1024^2 forward + quantise (u8 -> fp32); 8 frame sets = 40 MB, so it
         # is served from the 256 MiB Infinity Cache: the HBM fraction is not meaningful
         c2 = 1024

@@ -60,6 +60,43 @@ def pairs(rows, grid=None, name=None):
     return out
 
 
+def legs(rows, name=None, min_pairs=50):
+    """Runs of back-to-back pairs (round trip, fold, round trip, fold, ... with
+    nothing else in between on the queue): one per bench leg.  Per leg, over
+    its last 100 pairs (the leg's timed launches): mean period, round trip,
+    fold, and the two gaps (fold start - round-trip end, next round-trip
+    start - fold end)."""
+    by_q = {}
+    for r in rows:
+        by_q.setdefault(r["queue"], []).append(r)
+    out = []
+    for q in by_q.values():
+        found = [(i, q[i], q[i + 1]) for i in range(len(q) - 1)
+                 if "roundtrip_duo_kernel" in q[i]["name"] and "rt_spread_finish_kernel" in q[i + 1]["name"] and
+                 (name is None or name in q[i]["name"])]
+        cur = []
+        for x in found:
+            if cur and (x[0] != cur[-1][0] + 2 or x[1]["name"] != cur[-1][1]["name"]):
+                if len(cur) >= min_pairs:
+                    out.append(cur)
+                cur = []
+            cur.append(x)
+        if len(cur) >= min_pairs:
+            out.append(cur)
+    res = []
+    for leg in out:
+        tail = leg[-100:]
+        per = [(tail[k + 1][1]["t0"] - tail[k][1]["t0"]) / 1e3 for k in range(len(tail) - 1)]
+        res.append({"pairs": len(leg), "name": leg[0][1]["name"][:60],
+                    "period": statistics.fmean(per) if per else None,
+                    "rt": statistics.fmean((x[1]["t1"] - x[1]["t0"]) / 1e3 for x in tail),
+                    "fin": statistics.fmean((x[2]["t1"] - x[2]["t0"]) / 1e3 for x in tail),
+                    "gap_rt_fin": statistics.fmean((x[2]["t0"] - x[1]["t1"]) / 1e3 for x in tail),
+                    "gap_fin_next": statistics.fmean((tail[k + 1][1]["t0"] - tail[k][2]["t1"]) / 1e3
+                                                     for k in range(len(tail) - 1)) if len(tail) > 1 else None})
+    return res
+
+
 def summary(vals):
     vals = [v for v in vals if v is not None]
     if not vals:
@@ -96,6 +133,15 @@ def main():
         lines.append(f"Back-to-back pairs: mean period {statistics.fmean(p['period'] for p in bb):.2f} us against "
                      f"mean rt + fin {statistics.fmean(p['rt'] + p['fin'] for p in bb):.2f} us and mean "
                      f"rt + tail {statistics.fmean(p['rt'] + p['tail'] for p in bb):.2f} us.")
+    lg = legs(load(a.trace), a.name)
+    if lg:
+        lines += ["", "Per leg (runs of back-to-back pairs), over each leg's last 100 pairs, us:", "",
+                  "| pairs | period | round trip | fold | fold start - rt end | next rt start - fold end |",
+                  "|---|---|---|---|---|---|"]
+        for x in lg:
+            f = lambda v: "-" if v is None else f"{v:.2f}"  # noqa: E731
+            lines.append(f"| {x['pairs']} | {f(x['period'])} | {f(x['rt'])} | {f(x['fin'])} | {f(x['gap_rt_fin'])} |"
+                         f" {f(x['gap_fin_next'])} |")
     text = "\n".join(lines) + "\n"
     if a.out:
         with open(a.out, "w") as fh:
