@@ -255,3 +255,25 @@ def test_bench_nccl_process_group_at_world_size_1(tmp_path):
     assert c4["decode_int8_sets"] >= 2
     assert line["parity_spot_check"] is True
     assert line["provenance"]["lib_matches_sources"] is True
+    # the line says who took part in the gather
+    assert c4["rccl_nranks"] == 1 and c4["pg_world"] == 1 and c4["gather_bytes_expected"] == 0
+    assert line["c4_rccl_nranks"] == 1 and line["c4_pg_world"] == 1
+    # every kernel beside its copy ceiling, at the end of the line
+    ks = line["kernel_status"]
+    assert list(line)[-1] == "kernel_status"
+    for key in ("headline_fwd_u8_f32", "fwd_u8_i8", "inv_f32_f32", "dropin.dct_all_blocks_cuda", "c3.one_pass"):
+        us, ceil, frac, status = ks[key]
+        assert us > 0 and ceil > 0 and frac == round(ceil / us, 3) and status in ("done", "open")
+
+
+def test_bench_watchdog_exits_nonzero_after_the_headline_line(tmp_path):
+    """when the extras watchdog fires (a hung C4 gather, say), rank 0
+    still prints the headline line, with extras.error set, and the process
+    exits 3, not 0, so a caller that checks the exit code sees the hang."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5", "--warmup", "2",
+           "--size", "2048", "--sets", "4", "--no-cpu-baseline", "--sustain-s", "0", "--extras-timeout-s", "0.5"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 3, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert "watchdog" in line["extras"]["error"] and line["value"] > 0
