@@ -656,6 +656,7 @@ def bind_copy_ceiling(src, out0, out1=None, *, cap_waves: int = 0, stream=None):
     (hpdct_copy_ceiling, include/hpdct_baseline.h): the same bytes per pixel,
     no arithmetic, at most cap_waves resident one-wave workgroups per CU
     (0: no cap).  A zero-argument callable like bind().  Measurement only."""
+    _device_plane(src, "src", None, 0)
     n = src.numel()
     for name, t in (("out0", out0), ("out1", out1)):
         if t is not None:
@@ -676,6 +677,7 @@ def release_sums(sums_buf) -> None:
     """Return the library's 16 KiB spread slot kept for this sums buffer
     (hpdct_roundtrip_release_sums); call when no round trip with it is in
     flight (e.g. before freeing a ring of sums buffers)."""
+    _device_plane(sums_buf, "sums_buf", None, 3, (_torch().int64,))
     _check(load_library().hpdct_roundtrip_release_sums(ctypes.c_void_p(sums_buf.data_ptr())))
 
 

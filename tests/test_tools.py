@@ -58,7 +58,8 @@ def test_rt_pair_trace_reads_overlap_and_period(tmp_path):
     rows = ["Kind,Dispatch_Id,Queue_Id,Kernel_Name,Grid_Size_X,Start_Timestamp,End_Timestamp"]
     t = 1_000_000
     for i in range(4):
-        rows.append(f"KERNEL_DISPATCH,{2 * i},1,\"void hpdct::roundtrip_duo_kernel<true, 2>(...)\",2097152,{t},{t + 73000}")
+        rows.append(f"KERNEL_DISPATCH,{2 * i},1,\"void hpdct::roundtrip_duo_kernel<true, 2>(...)\",2097152,"
+                    f"{t},{t + 73000}")
         rows.append(f"KERNEL_DISPATCH,{2 * i + 1},1,\"void hpdct::rt_spread_finish_kernel<64>(...)\",64,"
                     f"{t + 70000},{t + 74900}")
         t += 75000
