@@ -79,6 +79,15 @@ void prod_i8_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
                        static_cast<const uint8_t*>(in), static_cast<int8_t*>(out), nullptr, c.g, nullptr, c.qp, 128.0f);
 }
 
+// C2's small frames: the octet kernel (8 tiles per wave) the library picks
+// below 8 sets per CU, at a chosen workgroup size (kVar bits 12..13)
+template <unsigned kVar>
+void oct_f32_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
+    hipLaunchKernelGGL((hpdct::fdct_octet_kernel<uint8_t, float, true, true, false, kVar>), octet_grid(c.g, kBlock<kVar>),
+                       dim3(kBlock<kVar>), 0, s, static_cast<const uint8_t*>(in), static_cast<float*>(out), nullptr,
+                       c.g, nullptr, c.qp, 128.0f);
+}
+
 // the tools-only tile kernel (kbench_variants.hpp), e.g. with ab::kVarPacked
 template <typename TOut, unsigned kVar>
 void ab_fwd(const void* in, void* out, const Ctx& c, hipStream_t s) {
@@ -568,6 +577,11 @@ int main(int argc, char** argv) {
         {"dropin", "dropin fwd f32 duo b64 cap 10 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 10>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo b64 cap 12 w/cu", dropin_fwd_cap<kDuoVar | (1u << 12), 12>, 12, 4, true},
         {"dropin", "dropin fwd f32 duo library again", dropin_fwd_cap<kDuoVar, 0>, 12, 4, true},
+        {"c2oct", "octet 256-thread WGs (library)", oct_f32_fwd<kOctVar<float> | kVarFastDiv>, 5, 4, true},
+        {"c2oct", "octet 512-thread WGs", oct_f32_fwd<(kOctVar<float> | kVarFastDiv) | (2u << 12)>, 5, 4, true},
+        {"c2oct", "octet 1024-thread WGs", oct_f32_fwd<(kOctVar<float> | kVarFastDiv) | (3u << 12)>, 5, 4, true},
+        {"c2oct", "octet 256-thread WGs again", oct_f32_fwd<kOctVar<float> | kVarFastDiv>, 5, 4, true},
+        {"c2oct", "tile 1024-thread WGs (the library's above 8 sets/CU)", prod_f32_fwd<((kProdVar<uint8_t, float> | kVarFastDiv | kVarJpegQ) & ~(3u << 12)) | (3u << 12)>, 5, 4, true},
         {"dropcap", "dropin uncapped (round 5)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0>, 12, 4, true},
         {"dropcap", "dropin b64 cap 10", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10>, 12, 4, true},
         {"dropcap", "dropin b64 cap 8", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 8>, 12, 4, true},
