@@ -56,6 +56,8 @@ __device__ __forceinline__ float* octet_slot() {
 // 64-entry table (+ optional second table) copied to LDS once per workgroup.
 template <unsigned kVar, int kTables>
 __device__ __forceinline__ const float* stage_tables(const Mat64& a, const Mat64* b) {
+    // threads 64..127 stage the second table
+    static_assert(kTables == 1 || kBlock<kVar> >= 128, "two tables need workgroups of at least 128 threads");
     __shared__ __attribute__((aligned(16))) float tab[kTables * 64];
     const uint32_t t = threadIdx.x;
     if (t < 64u) tab[t] = a.v[t];
