@@ -186,9 +186,10 @@ hpdct_status hpdct_roundtrip_u8_accumulate(const uint8_t* d_image, float* d_coef
 
 /* Return the spread slot kept for d_sums (16 KiB of device memory) to the
  * library, e.g. before freeing a ring of per-frame sums structs.  Call it when
- * no round trip with d_sums is in flight; a later round trip with the same
- * pointer takes a slot again.  A pointer without a slot (or NULL) is a no-op.
- * No reference counterpart. */
+ * no round trip with d_sums is in flight and no captured HIP graph that uses
+ * d_sums will be replayed (the slot may go to another pointer); a later round
+ * trip with the same pointer takes a slot again.  A pointer without a slot (or
+ * NULL) is a no-op.  No reference counterpart. */
 hpdct_status hpdct_roundtrip_release_sums(const hpdct_roundtrip_sums* d_sums);
 
 /* A list of independent device frames in as few launches as possible (config
