@@ -88,3 +88,30 @@ def test_frames_on_a_side_stream(hp, dev):
     s.synchronize()
     for x, y in zip(frames, outs):
         assert torch.equal(_bits(hp.forward(x)), _bits(y))
+
+
+@pytest.mark.parametrize("pattern", ["u8_f32", "u8_i8", "f32_f32", "f32_f32_f32inplace", "u8_f32_u8", "u8_f32_f32"])
+@pytest.mark.parametrize("cap", [0, 4])
+def test_copy_ceiling_moves_the_kernels_bytes(hp, dev, pattern, cap):
+    """hpdct_copy_ceiling (include/hpdct_baseline.h), the ceiling bench.py puts
+    beside every kernel, really reads and writes every byte it is charged for:
+    each output element is the input element converted (u8 -> f32 exactly,
+    f32 -> 1 B by truncation of the value), the in-place write-back included."""
+    import torch
+    n = 2048 * 37
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    src_u8 = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=gen).to(dev)
+    src_f32 = src_u8.float()
+    kinds = pattern.split("_")
+    src = src_u8 if kinds[0] == "u8" else src_f32.clone()
+    dt = {"u8": torch.uint8, "i8": torch.int8, "f32": torch.float32, "f32inplace": torch.float32}
+    o0 = torch.full((n,), 77, dtype=dt[kinds[1]], device=dev)
+    o1 = None
+    if len(kinds) > 2:
+        o1 = src if kinds[2] == "f32inplace" else torch.full((n,), 77, dtype=dt[kinds[2]], device=dev)
+    hp.bind_copy_ceiling(src, o0, o1, cap_waves=cap)()
+    torch.cuda.synchronize()
+    want = {torch.float32: src_f32, torch.uint8: src_u8, torch.int8: src_u8.view(torch.int8)}
+    assert torch.equal(o0, want[o0.dtype])
+    if o1 is not None:
+        assert torch.equal(o1, want[o1.dtype])
