@@ -216,6 +216,11 @@ int main(int argc, char** argv) {
         {"fold", "duo no sums", duo_sp<false, 256, 6>, false},
         {"fold", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
         {"fold", "duo + sums, fold in the kernel again", duo_kfold<0>, true},
+        {"finish", "duo + sums, atomic fold kernel (product)", duo_sp<true, 256, 6>, true},
+        {"finish", "duo + sums, plain-load fold kernel (round 5)", duo_fin<2>, true},
+        {"finish", "duo + sums, no fold kernel (timing)", duo_fin<1>, false},
+        {"finish", "duo + sums, atomic fold kernel again", duo_sp<true, 256, 6>, true},
+        {"finish", "duo + sums, plain-load fold kernel again", duo_fin<2>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
