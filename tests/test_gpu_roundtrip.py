@@ -476,3 +476,19 @@ def test_sse_f32_is_the_four_chain_definition(hp, oracle, dev, mapping, h, w):
         assert got["sse_f32"] * 65536 == want
     assert acc["sse_f32"] * 65536 == 2 * want
     assert acc["sse_u8"] == 2 * s8["sse_u8"] and acc["sum_x2"] == 2 * s8["sum_x2"]
+
+
+def test_roundtrip_beyond_the_duo_width_bound(hp, oracle, dev):
+    """the duo round trip addresses a wave's rows with 32-bit
+    byte offsets, valid below 2^22 pixels of width; a wider frame (here
+    2^22 + 256 px, a multiple of 256 that would otherwise take the duo
+    kernel) must take the tile kernel and stay bit-exact, sums included."""
+    import torch
+    w = (1 << 22) + 256
+    img = np.random.default_rng(123).integers(0, 256, (8, w), dtype=np.uint8)
+    q, r, r8, sums = expected(oracle, img)
+    coef, rec8, got = hp.roundtrip(to_dev(img, dev), recon_dtype=torch.uint8, sums=True)
+    assert bits_equal(to_host(coef), q)
+    assert np.array_equal(to_host(rec8), r8)
+    assert got["sum_x2"] == sums["sum_x2"] and got["sse_u8"] == sums["sse_u8"]
+    assert got["sse_f32"] * 65536 == oracle.rt_sse_f32_fx(img, r)
