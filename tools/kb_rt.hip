@@ -121,6 +121,17 @@ void duo_kfold(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hi
                        dim3(256), 0, s, img, coef, recon, g_spread, c.sums, c.g, c.qp, kMode);
 }
 
+// the bench's sums-ring leg: one spread slot per ring entry (a library slot per
+// caller sums pointer), kRing entries used in turn; kAcc: the fold adds
+int g_ring_k = 0;
+template <int kRing, int kAcc>
+void duo_ring(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    unsigned long long* const slot = g_spread + (size_t)(g_ring_k++ % kRing) * (kRtSpreadBytes / 8);
+    hipLaunchKernelGGL((roundtrip_duo_kernel<true, 2, kRtReconU8, true, 256, 6>), roundtrip_duo_grid(c.g, 256),
+                       dim3(256), 0, s, img, coef, recon, reinterpret_cast<RtSums*>(slot), c.g, c.qp);
+    hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, slot, kAcc);
+}
+
 // the tile kernel with the product's sums path (spread sub-slot 0 + finish)
 template <bool kStats>
 void tile_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
@@ -221,6 +232,13 @@ int main(int argc, char** argv) {
         {"finish", "duo + sums, no fold kernel (timing)", duo_fin<1>, false},
         {"finish", "duo + sums, atomic fold kernel again", duo_sp<true, 256, 6>, true},
         {"finish", "duo + sums, plain-load fold kernel again", duo_fin<2>, true},
+        {"ring", "duo + sums, one slot (product)", duo_sp<true, 256, 6>, true},
+        {"ring", "duo + sums, ring of 100 slots", duo_ring<100, 0>, true},
+        {"ring", "duo + sums, one slot, accumulate", duo_ring<1, 1>, false},
+        {"ring", "duo + sums, ring of 100 slots, accumulate", duo_ring<100, 1>, false},
+        {"ring", "duo + sums, ring of 16 slots", duo_ring<16, 0>, true},
+        {"ring", "duo + sums, one slot (product) again", duo_sp<true, 256, 6>, true},
+        {"ring", "duo + sums, ring of 100 slots again", duo_ring<100, 0>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
@@ -300,16 +318,20 @@ int main(int argc, char** argv) {
         }
     }
 
+    // KB_REC_BUFS=n: the reconstructions rotate over n planes instead of one per
+    // set (the bench's C3 legs rotate two)
+    const int nrec = getenv("KB_REC_BUFS") ? std::max(1, std::min(nsets, atoi(getenv("KB_REC_BUFS")))) : nsets;
+    printf("reconstruction planes: %d\n", nrec);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     std::vector<std::vector<float>> us(vars.size());
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vars.size(); ++v) {
-            for (int w = 0; w < 2 * nsets; ++w) vars[v].fn(img[w % nsets], coef[w % nsets], rec[w % nsets], c, 0);
+            for (int w = 0; w < 2 * nsets; ++w) vars[v].fn(img[w % nsets], coef[w % nsets], rec[w % nrec], c, 0);
             for (int i = 0; i < iters; i += nsets) {
                 CK(hipEventRecord(a, 0));
-                for (int k = 0; k < nsets; ++k) vars[v].fn(img[k], coef[k], rec[k], c, 0);
+                for (int k = 0; k < nsets; ++k) vars[v].fn(img[k], coef[k], rec[k % nrec], c, 0);
                 CK(hipEventRecord(b, 0));
                 CK(hipEventSynchronize(b));
                 float ms = 0;
