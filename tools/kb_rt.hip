@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "hpdct_launch.hpp"
 #include "kbench_rtduo_pk.hpp"
 #include "kbench_rtfold.hpp"
 
@@ -132,6 +133,18 @@ void duo_ring(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hip
     hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, slot, kAcc);
 }
 
+// round 6: the duo round trip under a residency cap (dynamic-LDS reservation,
+// residency_cap_lds): at most kWgs 256-thread workgroups (4 waves) per CU; the
+// kernel's registers allow 6 (24 waves per CU)
+template <bool kStats, int kWgs>
+void duo_cap(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    auto kern = roundtrip_duo_kernel<kStats, 2, kRtReconU8, true, 256, 6>;
+    static const size_t dyn = residency_cap_lds(static_lds_of(kern), kWgs);
+    RtSums* const sp = reinterpret_cast<RtSums*>(kStats ? g_spread : nullptr);
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256), dim3(256), dyn, s, img, coef, recon, sp, c.g, c.qp);
+    if (kStats) hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+}
+
 // the tile kernel with the product's sums path (spread sub-slot 0 + finish)
 template <bool kStats>
 void tile_sp(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
@@ -239,6 +252,17 @@ int main(int argc, char** argv) {
         {"ring", "duo + sums, ring of 16 slots", duo_ring<16, 0>, true},
         {"ring", "duo + sums, one slot (product) again", duo_sp<true, 256, 6>, true},
         {"ring", "duo + sums, ring of 100 slots again", duo_ring<100, 0>, true},
+        {"rtcap", "duo + sums (product, uncapped: 6 WGs/CU)", duo_sp<true, 256, 6>, true},
+        {"rtcap", "duo + sums, cap 5 WGs (20 waves) per CU", duo_cap<true, 5>, true},
+        {"rtcap", "duo + sums, cap 4 WGs (16 waves) per CU", duo_cap<true, 4>, true},
+        {"rtcap", "duo + sums, cap 3 WGs (12 waves) per CU", duo_cap<true, 3>, true},
+        {"rtcap", "duo no sums (uncapped)", duo_sp<false, 256, 6>, false},
+        {"rtcap", "duo no sums, cap 5 WGs per CU", duo_cap<false, 5>, false},
+        {"rtcap", "duo no sums, cap 4 WGs per CU", duo_cap<false, 4>, false},
+        {"rtcap", "duo no sums, cap 3 WGs per CU", duo_cap<false, 3>, false},
+        {"rtcap", "duo + sums (product) again", duo_sp<true, 256, 6>, true},
+        {"rtcap", "duo + sums, cap 5 WGs again", duo_cap<true, 5>, true},
+        {"rtcap", "duo + sums, cap 4 WGs again", duo_cap<true, 4>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
