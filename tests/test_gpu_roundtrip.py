@@ -165,10 +165,12 @@ def test_roundtrip_in_a_hip_graph(hp, oracle, dev):
 
 def test_roundtrip_sums_slots_many_buffers(hp, oracle, dev):
     """hpdct_roundtrip_u8's sums slots (hpdct_roundtrip.hip): one per sums
-    pointer, handed out from zeroed 1024-slot chunks and left zero by every
-    launch.  1100 distinct sums buffers (more than one chunk) each get the
+    pointer, handed out from zeroed 256-slot (4 MiB) chunks and left zero by
+    every launch's fold.  1100 distinct sums buffers (five chunks) each get the
     frame's totals, then another frame's on reuse; an accumulate launch on a
-    slotted buffer adds into the buffer itself and leaves the slot alone."""
+    slotted buffer goes through the same slot and its fold adds the frame's
+    sums to what the buffer holds; an overwrite after it writes the totals
+    again."""
     import torch
     a = oracle.rand_u8(64 * 128, 41).reshape(64, 128)
     b = oracle.rand_u8(72 * 256, 42).reshape(72, 256)
@@ -201,8 +203,8 @@ def test_roundtrip_sums_slots_many_buffers(hp, oracle, dev):
 
 
 def test_roundtrip_accumulate_adds_into_caller_zeroed_sums(hp, oracle, dev):
-    """hpdct_roundtrip_u8_accumulate: one kernel; each frame's sums are added to
-    the caller's struct.  A zeroed ring of per-frame slots gives the per-frame
+    """hpdct_roundtrip_u8_accumulate: the round trip and its fold, which adds
+    each frame's sums to the caller's struct.  A zeroed ring of per-frame slots gives the per-frame
     totals; two frames sharing a slot give the sum of both (exact integer
     fields, sse_f32 to the fixed-point unit); coefficients and reconstruction
     are the same bits as hpdct_roundtrip_u8."""
@@ -478,17 +480,23 @@ def test_sse_f32_is_the_four_chain_definition(hp, oracle, dev, mapping, h, w):
     assert acc["sse_u8"] == 2 * s8["sse_u8"] and acc["sum_x2"] == 2 * s8["sum_x2"]
 
 
-def test_roundtrip_beyond_the_duo_width_bound(hp, oracle, dev):
+@pytest.mark.parametrize("recon", ["u8", "f32"])
+def test_roundtrip_beyond_the_duo_width_bound(hp, oracle, dev, recon):
     """the duo round trip addresses a wave's rows with 32-bit
     byte offsets, valid below 2^22 pixels of width; a wider frame (here
     2^22 + 256 px, a multiple of 256 that would otherwise take the duo
-    kernel) must take the tile kernel and stay bit-exact, sums included."""
+    kernel) must take the tile kernel and stay bit-exact, sums included, with
+    either reconstruction."""
     import torch
     w = (1 << 22) + 256
     img = np.random.default_rng(123).integers(0, 256, (8, w), dtype=np.uint8)
     q, r, r8, sums = expected(oracle, img)
-    coef, rec8, got = hp.roundtrip(to_dev(img, dev), recon_dtype=torch.uint8, sums=True)
+    rdt = torch.uint8 if recon == "u8" else torch.float32
+    coef, rec, got = hp.roundtrip(to_dev(img, dev), recon_dtype=rdt, sums=True)
     assert bits_equal(to_host(coef), q)
-    assert np.array_equal(to_host(rec8), r8)
+    if recon == "u8":
+        assert np.array_equal(to_host(rec), r8)
+    else:
+        assert bits_equal(to_host(rec), r)
     assert got["sum_x2"] == sums["sum_x2"] and got["sse_u8"] == sums["sse_u8"]
     assert got["sse_f32"] * 65536 == oracle.rt_sse_f32_fx(img, r)
