@@ -53,7 +53,7 @@ HEADLINE_LEAD_S = 0.02         # the headline's warm-up reaches at least this mu
 MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MI355X_MICROARCH.md)
 INPUT_FOOTPRINT = 4 * MALL_BYTES  # rotating inputs must total at least this
 WATCHDOG_EXIT = 3              # exit code when the extras watchdog fired (headline line printed)
-CEIL_CAPS = (0, 4, 8, 12, 16)  # residency caps (waves per CU) the copy ceilings are timed at; 0 = none
+CEIL_CAPS = (0, 4, 6, 7, 8, 10, 12, 16, 20, 24)  # residency caps (waves per CU) of the copy ceilings; 0 = none
 DONE_FRAC = 0.9                # a kernel at >= this fraction of its copy ceiling is "done"
 
 
