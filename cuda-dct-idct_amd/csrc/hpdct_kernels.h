@@ -87,6 +87,15 @@ hipError_t launch_rt_finish(RtSums* dst, unsigned long long* spread, bool accumu
 // (hpdct_roundtrip_release_sums); false when the pointer had none
 bool release_sums_slot(const void* sums);
 
+// uint8 -> quantised fp32 forward on the two-lanes-per-tile mapping (round 6;
+// fdct_duo_u8_kernel, hpdct_rt_duo.hpp): qmode 1 or 2, built-in T, level
+// shift 128, tiles_x a multiple of 32, width below 2^22 px.  kDuoFwdBlock-thread
+// workgroups, at most kDuoFwdCapWgs resident per CU (16 waves); AUTO takes it
+// from kDuoFwdMinWavesPerCU of its 32-tile waves per CU (launch_fdct_impl).
+constexpr uint32_t kDuoFwdBlock = 256, kDuoFwdCapWgs = 4, kDuoFwdMinWavesPerCU = 4;
+hipError_t launch_fdct_duo_u8(const uint8_t* img, float* coef, const TileGrid& g, const QParams& qp, int qmode,
+                              hipStream_t s);
+
 // A list of frames per launch (hpdct_forward_frames): up to kMaxFramesPerLaunch
 // device pointer pairs travel in the kernel arguments (1 KiB).
 constexpr int kMaxFramesPerLaunch = 64;

@@ -7,6 +7,7 @@
 #include "hpdct_kernels_impl.hpp"
 #include "hpdct_octet.hpp"
 #include "hpdct_duo.hpp"
+#include "hpdct_residency.hpp"
 
 namespace hpdct {
 
@@ -34,52 +35,12 @@ inline dim3 grid_for(const TileGrid& g, bool persist, uint32_t cus, uint32_t blo
 // residency and at 0.75-0.80 with 12-4 waves per CU (tools/kbench3 "occpat",
 // profiles/r03/m/).  The arithmetic needs more than one wave per SIMD to issue
 // at full rate, so the u8 -> fp32 tile kernel runs in one-wave workgroups with
-// at most kF32CapWavesPerCU resident per CU.  The cap is set by reserving
-// dynamic LDS the kernel does not use: a workgroup that holds more than
-// 1/(k+1) of the CU's LDS leaves room for at most k.  The LDS size is the
-// device's own (hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, 160 KiB on
-// gfx950 per MI355X_MICROARCH.md), so the caps keep their meaning on a part
-// with another LDS size.
-constexpr size_t kLdsPerCUDefault = 160u * 1024u;
+// at most kF32CapWavesPerCU resident per CU.  The cap is a
+// dynamic-LDS reservation (hpdct_residency.hpp).
 // 10 in round 3; 7 since round 4: 56.9-57.1 against 57.7-58.4 us at 8192^2
 // with the per-position quantiser (profiles/r04/b/kb3_jqcap_8192.log; 6 waves
 // per CU: 64.8 us, profiles/r04/a/kb3_jqf_8192.log)
 constexpr uint32_t kF32CapWavesPerCU = 7;
-
-// A device attribute of the current device, cached per thread and device.
-template <hipDeviceAttribute_t kAttr>
-inline int device_attr(int fallback) {
-    static thread_local int cached_dev = -1;
-    static thread_local int cached = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return fallback;
-    if (dev != cached_dev) {
-        int v = 0;
-        cached = hipDeviceGetAttribute(&v, kAttr, dev) == hipSuccess && v > 0 ? v : fallback;
-        cached_dev = dev;
-    }
-    return cached;
-}
-inline uint32_t device_cus() {
-    return static_cast<uint32_t>(device_attr<hipDeviceAttributeMultiprocessorCount>(256));
-}
-inline size_t device_lds_per_cu() {
-    return static_cast<size_t>(
-        device_attr<hipDeviceAttributeMaxSharedMemoryPerMultiprocessor>(static_cast<int>(kLdsPerCUDefault)));
-}
-
-// dynamic LDS bytes for at most `wgs` resident workgroups per CU of a kernel
-// that has `static_bytes` of its own (0 when no reservation is needed)
-inline size_t residency_cap_lds(size_t static_bytes, uint32_t wgs) {
-    if (wgs == 0) return 0;
-    const size_t per = (device_lds_per_cu() / wgs) & ~static_cast<size_t>(511);
-    return per > static_bytes ? per - static_bytes : 0;
-}
-template <typename K>
-size_t static_lds_of(K kern) {
-    hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kern)) == hipSuccess ? a.sharedSizeBytes : 0;
-}
 
 // Product variant choice (measured on MI355X, tools/kbench.hip).
 //
@@ -273,6 +234,18 @@ hipError_t rowfirst_duo_go(const float* src, float* out, float* wb, const TileGr
     return hipGetLastError();
 }
 
+// uint8 -> quantised fp32 (verified quotient, built-in T, shift 128) on the
+// duo mapping (launch_fdct_duo_u8): whole 32-tile runs, widths below 2^22 px,
+// from kDuoFwdMinWavesPerCU of its waves per CU in AUTO (below that, 1024^2
+// and smaller, the octet kernel is as fast); forced "duo" takes it at any
+// size, forced "tile" or "octet" never.
+inline bool duo_fwd_u8_fits(const TileGrid& g) {
+    const int m = mapping_mode();
+    if (m == HPDCT_MAPPING_TILE || m == HPDCT_MAPPING_OCTET) return false;
+    if (g.tiles_x % 32u != 0u || g.width >= (uint64_t(1) << 22)) return false;
+    return m == HPDCT_MAPPING_DUO || g.ntiles / 32u >= kDuoFwdMinWavesPerCU * device_cus();
+}
+
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
 hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const TileGrid& g, const float* t_dev,
                             const QParams& q, float shift, int qmode, bool row_first, hipStream_t s) {
@@ -293,6 +266,9 @@ hipError_t launch_fdct_impl(const TIn* img, TOut* out, float* shifted, const Til
         }
     }
     (void)row_first;
+    if constexpr (kFastDivOk && std::is_same_v<TOut, float>) {
+        if (fastdiv && shift == 128.0f && duo_fwd_u8_fits(g)) return launch_fdct_duo_u8(img, out, g, q, qmode, s);
+    }
     constexpr bool kF32 = std::is_same_v<TIn, float> && std::is_same_v<TOut, float>;
     const Mapping map = pick_mapping(g, kF32);
     if constexpr (kF32) {

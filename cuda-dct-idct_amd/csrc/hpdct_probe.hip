@@ -120,9 +120,15 @@ hipError_t launch_copy_ceiling(const void* in, int in_bytes, void* o0, int o0_by
                          : copy_ceiling_o1<4, 4>(in, o0, o1, o1_bytes, n, cap_waves, s);
 }
 
-// The (grid, workgroup) the uint8 -> fp32 forward launches for g
-// (launch_fdct_impl -> fdct_octet_go / fdct_tile_go), without its residency cap.
+// The (grid, workgroup) the uint8 -> fp32 forward with the default table
+// launches for g (launch_fdct_impl -> launch_fdct_duo_u8 / fdct_octet_go /
+// fdct_tile_go), without its residency cap.
 void forward_u8_f32_shape(const TileGrid& g, dim3& grid, dim3& block) {
+    if (duo_fwd_u8_fits(g)) {
+        const uint32_t waves = (g.ntiles + 31u) / 32u, per = kDuoFwdBlock / 64u;
+        grid = dim3((waves + per - 1u) / per), block = dim3(kDuoFwdBlock);
+        return;
+    }
     if (pick_mapping(g, false) == Mapping::kOctet) {
         constexpr unsigned kV = kOctVar<float>;
         grid = octet_grid(g, kBlock<kV>), block = dim3(kBlock<kV>);

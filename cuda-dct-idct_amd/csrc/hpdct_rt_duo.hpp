@@ -405,6 +405,24 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
     }
 }
 
+// The forward alone on the duo mapping (round 6): uint8 frame -> quantised
+// fp32 coefficients.  It is the round trip's body without a reconstruction or
+// sums, whose inverse the compiler then drops (583 VALU and 20 lane swaps per
+// 32-tile wave, 58 VGPRs, against 992 and 52 for the round trip with a uint8
+// reconstruction): same loads, chains, quotient forms and re-staged 1 KiB
+// stores, so the same bits as the tile kernel's forward.  Launched in
+// kDuoFwdBlock-thread workgroups at most kDuoFwdCapWgs resident per CU
+// (launch_fdct_duo_u8): 8192^2 53.0 us against 56.1 for the tile kernel at its
+// cap, 2048 x 16384 (the C4 8-way slab) 28.4 against 32.8, 2048^2 5.3 against
+// 7.8 (octet), 1024^2 equal (tools/kb_rt groups fwdduo / fwdcap,
+// profiles/r06/kb_rt_fwdcap_*.log).
+template <int kQMode>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void fdct_duo_u8_kernel(
+    const uint8_t* __restrict__ img, float* __restrict__ coef, TileGrid g, QParams qp) {
+    uint32_t wave;
+    (void)rt_duo_waves<false, kQMode, kRtReconNone, true, 256, 1>(img, coef, nullptr, g, qp, wave);
+}
+
 inline dim3 roundtrip_duo_grid(const TileGrid& g, uint32_t block = 256, uint32_t sets = 1) {
     const uint32_t runs = (g.ntiles + kRtDuoTiles - 1u) / kRtDuoTiles, per = block / 64u;
     const uint32_t waves = (runs + sets - 1u) / sets;

@@ -49,7 +49,8 @@ def pick(d, needle, exclude=(), grid=None):
 # kernel key -> (name needle, exclude, read width, write width, B/px read, B/px written); a write
 # width may be a {width: B/px} mix, calibrated per part (the round trip stores fp32 rows and u8 rows)
 KERNELS = {
-    "fdct_u8_f32": ("fdct_kernel<unsigned char, float, true, true, false", (), "x2", "x4nt", 1, 4),
+    # round 6: the headline runs on the duo forward (hpdct_rt_duo.hpp fdct_duo_u8_kernel)
+    "fdct_u8_f32": ("fdct_duo_u8_kernel<2>", (), "x2", "x4nt", 1, 4),
     "fdct_u8_i8": ("fdct_kernel<unsigned char, signed char, true, true, false", (), "x2", "x2nt", 1, 1),
     "fdct_f32_f32_duo_runtimeT": ("fdct_duo_kernel<true, false, false", (), "x4", "x4nt", 4, 4),
     "idct_f32_f32_duo": ("idct_duo_kernel<true, true", ("unsigned char",), "x4", "x4nt", 4, 4),
@@ -100,6 +101,7 @@ def main():
             write_b = kw * 1024 * scale[ww]
         alg = (rb + wb) * n * n
         kernels[key] = {
+            "kernel": needle,
             "size": n,
             "fetch_size_kib_raw": kf, "write_size_kib_raw": kw,
             "read_width": rw, "write_width": ww,

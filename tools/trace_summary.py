@@ -5,10 +5,12 @@ launch shape, set beside the bench JSON line recorded in the same session.
   python tools/trace_summary.py <kernel_trace.csv> [--bench <bench.json>]
          [--warmup W] [--steps K] [--out summary.md]
 
-The bench's headline kernel (fdct_kernel<u8, f32, ...> at the 8192^2 grid) is
-also launched later by the round-trip extra at the same shape, so the
-headline's own launches are picked by dispatch order: launches [W, W+K) of
-that group are the timed region (bench.py: W warm-up, then exactly K).
+The bench's headline kernel (fdct_duo_u8_kernel<2> since round 6, before it
+fdct_kernel<u8, f32, ...>, at the 8192^2 grid) is also launched later by
+other extras at the same shape, so the headline's own launches are picked by
+dispatch order: after W warm-up launches and the bench's untimed lead-in
+(`warmup_lead_in_launches` of the bench line, when --bench is given), the
+next K are the timed region.
 Every other group is summarised whole (count, mean, median, min, max) and
 over its last 100 launches (the extras' timed region).
 """
@@ -60,8 +62,9 @@ def main():
     ap.add_argument("--bench", help="file holding the bench JSON line of the same session")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--headline-grid", type=int, default=(8192 * 8192 // 64 // 64) * 64,
-                    help="threads of the headline launch (one lane per 64-tile set lane)")
+    ap.add_argument("--headline-grid", type=int, default=(8192 * 8192 // 64 // 32) * 64,
+                    help="threads of the headline launch (duo forward: one wave per 32 tiles; the round-5 tile "
+                         "kernel: (8192*8192//64//64)*64)")
     ap.add_argument("--out")
     a = ap.parse_args()
     rows = load(a.trace)
@@ -79,24 +82,28 @@ def main():
         summary["groups"].append(st)
         lines.append(f"| `{name}` | {grid} | {wg} | {rs[0]['vgpr']} | {st['calls']} | {st['mean_us']} | "
                      f"{st['median_us']} | {st['min_us']} | {st['max_us']} | {st['last100_mean_us']} |")
-    head = [r for r in rows if r["name"].startswith("fdct_kernel<u8,f32,") and r["grid"] == a.headline_grid]
-    out = "\n".join(lines) + "\n"
-    if len(head) >= a.warmup + a.steps:
-        timed = [r["us"] for r in head[a.warmup:a.warmup + a.steps]]
-        hs = stats(timed)
-        summary["headline_timed"] = hs
-        out += (f"\nHeadline timed region (launches {a.warmup}..{a.warmup + a.steps - 1} of "
-                f"`{head[0]['name']}` at grid {a.headline_grid}): mean {hs['mean_us']} us, median "
-                f"{hs['median_us']}, min {hs['min_us']}, max {hs['max_us']}\n")
-        frac = 5 * 8192 * 8192 / (hs["mean_us"] * 1e-6) / 8e12
-        out += f"  -> 5 B/px x 8192^2 / mean = {frac:.4f} of 8 TB/s\n"
+    head = [r for r in rows if r["name"].startswith(("fdct_duo_u8_kernel<", "fdct_kernel<u8,f32,")) and
+            r["grid"] == a.headline_grid]
+    line = None
     if a.bench:
-        line = None
         with open(a.bench) as fh:
             for ln in fh:
                 ln = ln.strip()
                 if ln.startswith("{") and '"metric"' in ln:
                     line = json.loads(ln)
+    lead = int((line or {}).get("warmup_lead_in_launches", 0) or 0)
+    first = a.warmup + lead
+    out = "\n".join(lines) + "\n"
+    if len(head) >= first + a.steps:
+        timed = [r["us"] for r in head[first:first + a.steps]]
+        hs = stats(timed)
+        summary["headline_timed"] = hs
+        out += (f"\nHeadline timed region (launches {first}..{first + a.steps - 1} of "
+                f"`{head[0]['name']}` at grid {a.headline_grid}): mean {hs['mean_us']} us, median "
+                f"{hs['median_us']}, min {hs['min_us']}, max {hs['max_us']}\n")
+        frac = 5 * 8192 * 8192 / (hs["mean_us"] * 1e-6) / 8e12
+        out += f"  -> 5 B/px x 8192^2 / mean = {frac:.4f} of 8 TB/s\n"
+    if a.bench:
         if line:
             summary["bench"] = {"ms_per_step": line["ms_per_step"], "frac": line["roofline"]["frac"],
                                 "kernel_us_avg": line["roofline"]["kernel_us_avg"]}
