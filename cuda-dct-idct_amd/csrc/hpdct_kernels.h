@@ -109,6 +109,10 @@ struct FrameTable {
 template <typename TOut>
 hipError_t launch_fdct_frames(const FrameTable<TOut>& ft, int n, const TileGrid& g, const QParams& q, int qmode,
                               hipStream_t s);
+// the duo forward over such a list (fp32 out; the conditions of
+// launch_fdct_duo_u8, the size rule on the whole list)
+hipError_t launch_fdct_duo_u8_frames(const FrameTable<float>& ft, int n, const TileGrid& g, const QParams& qp,
+                                     int qmode, hipStream_t s);
 
 hipError_t launch_fill_hash(uint8_t* out, uint64_t n, uint64_t seed, uint64_t first, hipStream_t s);
 

@@ -239,11 +239,13 @@ hipError_t rowfirst_duo_go(const float* src, float* out, float* wb, const TileGr
 // from kDuoFwdMinWavesPerCU of its waves per CU in AUTO (below that, 1024^2
 // and smaller, the octet kernel is as fast); forced "duo" takes it at any
 // size, forced "tile" or "octet" never.
-inline bool duo_fwd_u8_fits(const TileGrid& g) {
+// frames: how many frames of g one launch covers (a frame list).
+inline bool duo_fwd_u8_fits(const TileGrid& g, uint32_t frames = 1) {
     const int m = mapping_mode();
     if (m == HPDCT_MAPPING_TILE || m == HPDCT_MAPPING_OCTET) return false;
     if (g.tiles_x % 32u != 0u || g.width >= (uint64_t(1) << 22)) return false;
-    return m == HPDCT_MAPPING_DUO || g.ntiles / 32u >= kDuoFwdMinWavesPerCU * device_cus();
+    return m == HPDCT_MAPPING_DUO ||
+           static_cast<uint64_t>(g.ntiles / 32u) * frames >= uint64_t(kDuoFwdMinWavesPerCU) * device_cus();
 }
 
 template <typename TIn, typename TOut, bool kQuant, bool kBuiltinT, bool kWriteback>
@@ -432,6 +434,9 @@ hipError_t launch_fdct_frames_impl(const FrameTable<TOut>& ft, int n, const Tile
     constexpr unsigned kBase = kProdVar<uint8_t, TOut>;
     constexpr unsigned kJ = kVarFastDiv | kVarJpegQ;
     if constexpr (std::is_same_v<TOut, float>) {
+        // the duo forward (round 6), as for one frame
+        if (qmode != 0 && duo_fwd_u8_fits(g, static_cast<uint32_t>(n)))
+            return launch_fdct_duo_u8_frames(ft, n, g, q, qmode, s);
         if (g.tiles_x % 64u != 0u)
             return qmode == 2   ? fdct_frames_go<kBase | kJ | kVarStraddle>(ft, n, g, q, s)
                    : qmode == 1 ? fdct_frames_go<kBase | kVarFastDiv | kVarStraddle>(ft, n, g, q, s)

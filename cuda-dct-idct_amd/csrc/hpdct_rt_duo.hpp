@@ -141,12 +141,19 @@ __device__ __forceinline__ void rt_duo_row_sums(uint2 w, const float (&r)[8], ui
 // Otherwise (ragged widths) per-lane validity and 32-B row stores.  Two
 // kernels, not a branch per wave: a runtime branch around the staging costs
 // the whole body ~16 VGPRs (94 against 78).
-template <bool kStats, int kQMode, int kRecon, bool kRun>
-__device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, float* __restrict__ coef,
+// TC: the coefficient plane's type, float (the reference's) or int8_t (the
+// wire format; forward only: no reconstruction, no sums).
+template <bool kStats, int kQMode, int kRecon, bool kRun, typename TC = float>
+__device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, TC* __restrict__ coef,
                                             void* __restrict__ recon, const DuoAddr& a, uint32_t h,
                                             const float (&tab)[2][64], float4* __restrict__ slots, f32x2& acc_f2,
                                             uint32_t& acc_xx, uint32_t& acc_xr, uint32_t& acc_rr) {
     constexpr bool kNT = true;
+    constexpr bool kI8 = std::is_same_v<TC, int8_t>;
+    // int8 coefficients hold the quantiser's values before the final trunc (the
+    // truncating convert does it), so D below is only right for fp32: the int8
+    // kernel must be forward only (the compiler then drops the inverse)
+    static_assert(!kI8 || (kRecon == kRtReconNone && !kStats), "int8 coefficients: forward only");
     const TSource<true, true> T(nullptr);  // built-in T, zero terms skipped (finite operands)
     const uint32_t lane = threadIdx.x & 63u;
     const uint8_t* const src = img + a.base;
@@ -207,16 +214,23 @@ __device__ __forceinline__ void rt_duo_body(const uint8_t* __restrict__ img, flo
                 } else {
                     m = h ? quantforms::jpeg_bias(ph) : quantforms::jpeg_bias(pl);
                 }
-                c[u] = __builtin_truncf(__builtin_fmaf(s, rv[u], signed_mag(m, s)));
+                const float b = __builtin_fmaf(s, rv[u], signed_mag(m, s));
+                c[u] = kI8 ? b : __builtin_truncf(b);
             } else {
                 const float q0v = s * rv[u];
                 const float e = __builtin_fmaf(-q0v, qv[u], s);
                 const float d = __builtin_fmaf(e, rv[u], q0v);
-                c[u] = __builtin_truncf(d + signed_half(d));
+                const float b = d + signed_half(d);
+                c[u] = kI8 ? b : __builtin_truncf(b);
             }
         });
         // coefficient row 2k+h
-        if constexpr (kRun) {
+        if constexpr (kI8) {
+            // the truncating convert straight into each byte; 8 B per lane: the
+            // wave's rows 2k and 2k+1 of its 32 tiles, two 256-B runs
+            const uint2 w = make_uint2(pack_biased_i8x4(c[0], c[1], c[2], c[3]), pack_biased_i8x4(c[4], c[5], c[6], c[7]));
+            if (kRun || a.valid) st<kNT>(reinterpret_cast<uint2*>(coef + a.base + a.off(row)), w);
+        } else if constexpr (kRun) {
             float4* const slot = slots + (k & 1) * 128;
             slot[2u * lane] = make_float4(c[0], c[1], c[2], c[3]);
             slot[2u * lane + 1u] = make_float4(c[4], c[5], c[6], c[7]);
@@ -318,8 +332,8 @@ struct DuoWaveSums {
 // The body both round-trip kernels share: the Q tables to LDS, the wave's
 // kSets runs of 32 tiles (a grid apart), and the wave's sums (kStats).
 // kSets: 32-tile runs per wave.
-template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT, int kSets>
-__device__ __forceinline__ DuoWaveSums rt_duo_waves(const uint8_t* __restrict__ img, float* __restrict__ coef,
+template <bool kStats, int kQMode, int kRecon, bool kRun, int kBlockT, int kSets, typename TC = float>
+__device__ __forceinline__ DuoWaveSums rt_duo_waves(const uint8_t* __restrict__ img, TC* __restrict__ coef,
                                                     void* __restrict__ recon, const TileGrid& g, const QParams& qp,
                                                     uint32_t& wave_out) {
     static_assert(kQMode == 1 || kQMode == 2, "duo round trip: verified quotient only");
@@ -353,7 +367,8 @@ __device__ __forceinline__ DuoWaveSums rt_duo_waves(const uint8_t* __restrict__ 
         const DuoAddr a{static_cast<uint64_t>(by) * 8u * g.width + static_cast<uint64_t>(bx) * 8u, lane_off, w32,
                         first + t < g.ntiles};
         f32x2 acc_f2 = {0.0f, 0.0f};  // the run's tile: this lane's two chains
-        rt_duo_body<kStats, kQMode, kRecon, kRun>(img, coef, recon, a, h, tab, slots, acc_f2, acc_xx, acc_xr, acc_rr);
+        rt_duo_body<kStats, kQMode, kRecon, kRun, TC>(img, coef, recon, a, h, tab, slots, acc_f2, acc_xx, acc_xr,
+                                                      acc_rr);
         if constexpr (kStats) {
             rt_sse_split(acc_f2.x, ok, f_hi, f_lo);
             rt_sse_split(acc_f2.y, ok, f_hi, f_lo);
@@ -416,11 +431,25 @@ __global__ __launch_bounds__(kBlockT) __attribute__((amdgpu_waves_per_eu(kWaves,
 // cap, 2048 x 16384 (the C4 8-way slab) 28.4 against 32.8, 2048^2 5.3 against
 // 7.8 (octet), 1024^2 equal (tools/kb_rt groups fwdduo / fwdcap,
 // profiles/r06/kb_rt_fwdcap_*.log).
-template <int kQMode>
+// TC int8_t: the int8 wire format, 8 B row stores (no LDS re-staging);
+// bit-exact but slower than the int8 tile kernel (8192^2 36.3 against 31.8 us,
+// tools/kb_rt group i8duo, profiles/r06/kb_rt_i8duo_*.log), so only the A/B
+// harness instantiates it.
+template <int kQMode, typename TC = float>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void fdct_duo_u8_kernel(
-    const uint8_t* __restrict__ img, float* __restrict__ coef, TileGrid g, QParams qp) {
+    const uint8_t* __restrict__ img, TC* __restrict__ coef, TileGrid g, QParams qp) {
     uint32_t wave;
-    (void)rt_duo_waves<false, kQMode, kRtReconNone, true, 256, 1>(img, coef, nullptr, g, qp, wave);
+    (void)rt_duo_waves<false, kQMode, kRtReconNone, true, 256, 1, TC>(img, coef, nullptr, g, qp, wave);
+}
+
+// The same forward over a list of frames of one shape (hpdct_forward_frames):
+// blockIdx.y picks the frame, whose pointers travel in the kernel arguments.
+template <int kQMode>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void fdct_duo_u8_frames_kernel(
+    FrameTable<float> ft, TileGrid g, QParams qp) {
+    uint32_t wave;
+    const uint32_t f = blockIdx.y;
+    (void)rt_duo_waves<false, kQMode, kRtReconNone, true, 256, 1>(ft.in[f], ft.out[f], nullptr, g, qp, wave);
 }
 
 inline dim3 roundtrip_duo_grid(const TileGrid& g, uint32_t block = 256, uint32_t sets = 1) {

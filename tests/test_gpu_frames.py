@@ -8,7 +8,10 @@ BIT, and sampled frames equal the CPU oracle (the checker only).  Cases: more
 than 64 frames (two launches, the second ragged), a width that is not a
 multiple of 512 px (the straddle-capable stores), the C2 1024^2 frame size in
 fp32 and int8, an input pool repeated across the list, and a custom integer
-quant table (the verified fast quotient) against an IEEE-division one.
+quant table (the verified fast quotient) against an IEEE-division one.  Since
+round 6 a large enough fp32 list of whole-run widths runs on the duo forward
+(1024^2 x 33, 256 x 2048 x 70 in two launches) while each frame alone takes
+the octet kernel: the two mappings must agree bit for bit.
 """
 import numpy as np
 import pytest
@@ -34,7 +37,7 @@ def _bits(t):
 
 
 @pytest.mark.parametrize("out_dtype", ["float32", "int8"])
-@pytest.mark.parametrize("h,w,n", [(64, 136, 70), (1024, 1024, 33), (48, 4096, 3), (8, 8, 1)])
+@pytest.mark.parametrize("h,w,n", [(64, 136, 70), (1024, 1024, 33), (48, 4096, 3), (8, 8, 1), (256, 2048, 70)])
 def test_frames_equal_per_frame_forward(hp, dev, out_dtype, h, w, n):
     import torch
     dt = getattr(torch, out_dtype)

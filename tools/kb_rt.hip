@@ -23,6 +23,19 @@
 using namespace hpdct;
 // the product's mapping switch lives in hpdct_api.cpp; the harness is AUTO
 int hpdct::mapping_mode() { return 0; }
+// the library's duo-forward launcher (hpdct_rt_duo.hip), which launch_fdct_impl calls
+template <int kQ>
+static hipError_t duo_fwd_lib(const uint8_t* img, float* coef, const TileGrid& g, const QParams& qp, hipStream_t s) {
+    auto* const kern = fdct_duo_u8_kernel<kQ>;
+    static const size_t st = static_lds_of(kern);
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(g, kDuoFwdBlock), dim3(kDuoFwdBlock),
+                       residency_cap_lds(st, kDuoFwdCapWgs), s, img, coef, g, qp);
+    return hipGetLastError();
+}
+hipError_t hpdct::launch_fdct_duo_u8(const uint8_t* img, float* coef, const TileGrid& g, const QParams& qp,
+                                     int qmode, hipStream_t s) {
+    return qmode == 2 ? duo_fwd_lib<2>(img, coef, g, qp, s) : duo_fwd_lib<1>(img, coef, g, qp, s);
+}
 
 #define CK(x)                                                                        \
     do {                                                                             \
@@ -164,6 +177,19 @@ void duo_fwd(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStream_
     auto kern = roundtrip_duo_kernel<false, 2, kRtReconNone, true, kB, 6>;
     static const size_t dyn = residency_cap_lds(static_lds_of(kern), kWgs);
     hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, kB), dim3(kB), dyn, s, img, coef, nullptr, nullptr, c.g, c.qp);
+}
+// round 6: the int8 wire format on the duo forward (the plane passed as
+// float* is written as px int8 bytes)
+void headline_i8_product(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStream_t s) {
+    (void)launch_fdct_impl<uint8_t, int8_t, true, true, false>(img, reinterpret_cast<int8_t*>(coef), nullptr, c.g,
+                                                               nullptr, c.qp, 128.0f, 2, false, s);
+}
+template <int kWgs>
+void duo_i8(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStream_t s) {
+    auto kern = fdct_duo_u8_kernel<2, int8_t>;
+    static const size_t dyn = residency_cap_lds(static_lds_of(kern), kWgs);
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256), dim3(256), dyn, s, img, reinterpret_cast<int8_t*>(coef),
+                       c.g, c.qp);
 }
 template <int kWgs>
 void duo_norecon(const uint8_t* img, float* coef, uint8_t* r, const Ctx& c, hipStream_t s) {
@@ -310,6 +336,14 @@ int main(int argc, char** argv) {
         {"fwdcap", "headline product again", headline_product, false, false},
         {"fwdcap", "duo fwd 256-thr, cap 4 WGs again", duo_fwd<256, 4>, false, false},
         {"fwdcap", "duo fwd 64-thr, cap 16 waves again", duo_fwd<64, 16>, false, false},
+        {"i8duo", "int8 product (tile, 20 waves/CU)", headline_i8_product, false, false},
+        {"i8duo", "int8 duo fwd, uncapped (6 WGs/CU)", duo_i8<0>, false, false},
+        {"i8duo", "int8 duo fwd, cap 5 WGs", duo_i8<5>, false, false},
+        {"i8duo", "int8 duo fwd, cap 4 WGs", duo_i8<4>, false, false},
+        {"i8duo", "int8 duo fwd, cap 3 WGs", duo_i8<3>, false, false},
+        {"i8duo", "int8 product again", headline_i8_product, false, false},
+        {"i8duo", "int8 duo fwd, uncapped again", duo_i8<0>, false, false},
+        {"i8duo", "int8 duo fwd, cap 5 WGs again", duo_i8<5>, false, false},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
@@ -349,7 +383,12 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> r0(px), r1(px);
         for (int s = 0; s < 2; ++s) {
             RtSums s0{}, s1{};
-            tile_rt<true>(img[s], coef[2], rec[2], c, 0);
+            if (only == "i8duo") {  // int8 variants: the reference is the int8 product, the rest of the plane 0xa5
+                CK(hipMemset(coef[2], 0xa5, px * 4));
+                headline_i8_product(img[s], coef[2], rec[2], c, 0);
+            } else {
+                tile_rt<true>(img[s], coef[2], rec[2], c, 0);
+            }
             CK(hipDeviceSynchronize());
             CK(hipMemcpy(c0.data(), coef[2], px * 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(r0.data(), rec[2], px, hipMemcpyDeviceToHost));
