@@ -191,6 +191,14 @@ void duo_i8(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStream_t
     hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256), dim3(256), dyn, s, img, reinterpret_cast<int8_t*>(coef),
                        c.g, c.qp);
 }
+// kSets runs of 32 tiles per wave (a grid apart), forward only
+template <int kSets, int kWgs>
+void duo_fwd_s(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStream_t s) {
+    auto kern = roundtrip_duo_kernel<false, 2, kRtReconNone, true, 256, 6, kSets>;
+    static const size_t dyn = residency_cap_lds(static_lds_of(kern), kWgs);
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256, kSets), dim3(256), dyn, s, img, coef, nullptr, nullptr,
+                       c.g, c.qp);
+}
 template <int kWgs>
 void duo_norecon(const uint8_t* img, float* coef, uint8_t* r, const Ctx& c, hipStream_t s) {
     duo_fwd<256, kWgs>(img, coef, r, c, s);
@@ -344,6 +352,14 @@ int main(int argc, char** argv) {
         {"i8duo", "int8 product again", headline_i8_product, false, false},
         {"i8duo", "int8 duo fwd, uncapped again", duo_i8<0>, false, false},
         {"i8duo", "int8 duo fwd, cap 5 WGs again", duo_i8<5>, false, false},
+        {"fwdsets", "product (duo fwd, 1 run/wave, cap 4 WGs)", headline_product, false, false},
+        {"fwdsets", "duo fwd, 2 runs/wave, cap 4 WGs", duo_fwd_s<2, 4>, false, false},
+        {"fwdsets", "duo fwd, 2 runs/wave, cap 3 WGs", duo_fwd_s<2, 3>, false, false},
+        {"fwdsets", "duo fwd, 2 runs/wave, cap 5 WGs", duo_fwd_s<2, 5>, false, false},
+        {"fwdsets", "duo fwd, 4 runs/wave, cap 4 WGs", duo_fwd_s<4, 4>, false, false},
+        {"fwdsets", "duo fwd, 1 run/wave, cap 4 WGs (kernel)", duo_fwd_s<1, 4>, false, false},
+        {"fwdsets", "product again", headline_product, false, false},
+        {"fwdsets", "duo fwd, 2 runs/wave, cap 4 WGs again", duo_fwd_s<2, 4>, false, false},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
