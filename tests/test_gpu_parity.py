@@ -37,9 +37,10 @@ def mismatches(a, b):
 
 @pytest.fixture(autouse=True, params=["tile", "octet", "duo"])
 def mapping(request, hp, monkeypatch):
-    """Every parity case runs under each forced work mapping (one, eight or,
-    for fp32 -> fp32, two lanes per tile); child processes inherit
-    HPDCT_MAPPING.  AUTO picks among these per frame size."""
+    """Every parity case runs under each forced work mapping (one, eight or
+    two lanes per tile; two: the fp32 -> fp32 kernels and, since round 6, the
+    uint8 -> quantised fp32 forward of whole 32-tile runs); child processes
+    inherit HPDCT_MAPPING.  AUTO picks among these per frame size."""
     monkeypatch.setenv("HPDCT_MAPPING", request.param)
     hp.set_mapping(request.param)
     yield request.param
