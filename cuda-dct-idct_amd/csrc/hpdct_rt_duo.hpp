@@ -51,6 +51,7 @@
 #pragma once
 
 #include "hpdct_octet.hpp"
+#include "hpdct_residency.hpp"
 #include "hpdct_roundtrip.hpp"
 
 namespace hpdct {
@@ -464,12 +465,25 @@ namespace rt_duo_detail {
 // (tiles_x a multiple of 32, launch_roundtrip checks): the kRun = false kernel
 // (ragged widths, 92 VGPRs) is slower than the tile kernel there (4096 x 4104:
 // 36.9 against 31.9 us with sums, profiles/r05/b/kb_rt_ragged.log).
+// Round 6: at most kDuoRtCapWgs workgroups (16 waves) per CU, by the
+// dynamic-LDS reservation, for the fp32 reconstruction and for every round
+// trip without sums: 8192^2 fp32 reconstruction + sums 100.2-100.3 against
+// 106.6-106.7 us uncapped, without sums 98.9 against 102.4; uint8
+// reconstruction without sums 67.2 against 68.4 (tools/kb_rt group f32cap,
+// profiles/r06/kb_rt_f32cap.log).  The uint8 reconstruction with sums (the C3
+// one pass) gains nothing from it (group rtcap) and stays uncapped.
 constexpr int kDuoRtBlock = 256, kDuoRtWaves = 6;
+constexpr uint32_t kDuoRtCapWgs = 4;
 template <bool kStats, int kQMode, int kRecon>
 hipError_t go(const uint8_t* img, float* coef, void* recon, unsigned long long* spread, const TileGrid& g,
               const QParams& qp, hipStream_t s) {
-    hipLaunchKernelGGL((roundtrip_duo_kernel<kStats, kQMode, kRecon, true, kDuoRtBlock, kDuoRtWaves>),
-                       roundtrip_duo_grid(g, kDuoRtBlock), dim3(kDuoRtBlock), 0, s, img, coef, recon,
+    auto* const kern = roundtrip_duo_kernel<kStats, kQMode, kRecon, true, kDuoRtBlock, kDuoRtWaves>;
+    size_t dyn = 0;
+    if constexpr (kRecon == kRtReconF32 || !kStats) {
+        static const size_t st = static_lds_of(kern);
+        dyn = residency_cap_lds(st, kDuoRtCapWgs);
+    }
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(g, kDuoRtBlock), dim3(kDuoRtBlock), dyn, s, img, coef, recon,
                        reinterpret_cast<RtSums*>(spread), g, qp);
     return hipGetLastError();
 }

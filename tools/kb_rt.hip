@@ -199,6 +199,17 @@ void duo_fwd_s(const uint8_t* img, float* coef, uint8_t*, const Ctx& c, hipStrea
     hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256, kSets), dim3(256), dyn, s, img, coef, nullptr, nullptr,
                        c.g, c.qp);
 }
+// the fp32-reconstruction round trip (+ sums + fold), capped; the recon plane
+// passed as uint8_t* holds px floats (group f32cap allocates them so; its
+// reconstruction check against the uint8 product is moot: run with KB_CONTINUE)
+template <bool kStats, int kWgs>
+void duo_f32rt(const uint8_t* img, float* coef, uint8_t* recon, const Ctx& c, hipStream_t s) {
+    auto kern = roundtrip_duo_kernel<kStats, 2, kRtReconF32, true, 256, 6>;
+    static const size_t dyn = residency_cap_lds(static_lds_of(kern), kWgs);
+    hipLaunchKernelGGL(kern, roundtrip_duo_grid(c.g, 256), dim3(256), dyn, s, img, coef, static_cast<void*>(recon),
+                       reinterpret_cast<RtSums*>(kStats ? g_spread : nullptr), c.g, c.qp);
+    if (kStats) hipLaunchKernelGGL(rt_spread_finish_kernel<>, dim3(1), dim3(64), 0, s, c.sums, g_spread, 0);
+}
 template <int kWgs>
 void duo_norecon(const uint8_t* img, float* coef, uint8_t* r, const Ctx& c, hipStream_t s) {
     duo_fwd<256, kWgs>(img, coef, r, c, s);
@@ -360,6 +371,16 @@ int main(int argc, char** argv) {
         {"fwdsets", "duo fwd, 1 run/wave, cap 4 WGs (kernel)", duo_fwd_s<1, 4>, false, false},
         {"fwdsets", "product again", headline_product, false, false},
         {"fwdsets", "duo fwd, 2 runs/wave, cap 4 WGs again", duo_fwd_s<2, 4>, false, false},
+        {"f32cap", "f32 recon + sums (product, uncapped)", duo_f32rt<true, 0>, true},
+        {"f32cap", "f32 recon + sums, cap 5 WGs", duo_f32rt<true, 5>, true},
+        {"f32cap", "f32 recon + sums, cap 4 WGs", duo_f32rt<true, 4>, true},
+        {"f32cap", "f32 recon + sums, cap 3 WGs", duo_f32rt<true, 3>, true},
+        {"f32cap", "f32 recon, no sums (uncapped)", duo_f32rt<false, 0>, false},
+        {"f32cap", "f32 recon, no sums, cap 4 WGs", duo_f32rt<false, 4>, false},
+        {"f32cap", "u8 recon, no sums (uncapped)", duo_sp<false, 256, 6>, false},
+        {"f32cap", "u8 recon, no sums, cap 4 WGs", duo_cap<false, 4>, false},
+        {"f32cap", "f32 recon + sums (product) again", duo_f32rt<true, 0>, true},
+        {"f32cap", "f32 recon + sums, cap 4 WGs again", duo_f32rt<true, 4>, true},
         {"ragged", "tile rt + sums, spread + finish", tile_sp<true>, true},
         {"ragged", "duo + sums, ragged kernel", duo_sp<true, 256, 5, false, false>, true},
         {"ragged", "duo no sums, ragged kernel", duo_sp<false, 256, 5, false, false>, false},
@@ -381,7 +402,7 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < px; ++i) h[i] = (uint8_t)(rand() % 256);
     for (int s = 0; s < nsets; ++s) {
         CK(hipMalloc(&img[s], px));
-        CK(hipMalloc(&rec[s], px));
+        CK(hipMalloc(&rec[s], px * (only == "f32cap" ? 4 : 1)));  // f32cap: fp32 reconstructions
         CK(hipMalloc(&coef[s], px * 4));
         if (s == 0) {
             CK(hipMemcpy(img[s], h.data(), px, hipMemcpyHostToDevice));
