@@ -590,6 +590,16 @@ int main(int argc, char** argv) {
         {"fwdcap", "fwd no wb uncapped (round 5)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0, false>, 8, 4, true},
         {"fwdcap", "fwd no wb b64 cap 10", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10, false>, 8, 4, true},
         {"fwdcap", "fwd no wb uncapped again", dropin_fwd_rt<kDuoVar | kVarFastDivChecked, 0, false>, 8, 4, true},
+        // round 6, after the duo forward's 16-wave cap: the fp32 duo forward in 256-thread workgroups
+        {"duocap16", "dropin b64 cap 10 (product)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10>, 12, 4, true},
+        {"duocap16", "dropin b64 cap 16", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 16>, 12, 4, true},
+        {"duocap16", "dropin b64 cap 6", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 6>, 12, 4, true},
+        {"duocap16", "dropin b256 cap 4 WGs", dropin_fwd_rt<(kDuoVar | kVarFastDivChecked) & ~(3u << 12), 4>, 12, 4, true},
+        {"duocap16", "dropin b256 cap 3 WGs", dropin_fwd_rt<(kDuoVar | kVarFastDivChecked) & ~(3u << 12), 3>, 12, 4, true},
+        {"duocap16", "fwd no wb b64 cap 10 (product)", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10, false>, 8, 4, true},
+        {"duocap16", "fwd no wb b256 cap 4 WGs", dropin_fwd_rt<(kDuoVar | kVarFastDivChecked) & ~(3u << 12), 4, false>, 8, 4, true},
+        {"duocap16", "dropin b64 cap 10 (product) again", dropin_fwd_rt<kDuoVar | kVarFastDivChecked | (1u << 12), 10>, 12, 4, true},
+        {"duocap16", "dropin b256 cap 4 WGs again", dropin_fwd_rt<(kDuoVar | kVarFastDivChecked) & ~(3u << 12), 4>, 12, 4, true},
         // round 4: the default JPEG table's per-position 3-op quantiser forms (kVarJpegQ) against the
         // verified 6-op form, in the product's dispatch, and the headline cap re-swept with them
         {"jq", "fwd u8->f32 library cap 10 (6-op)", prod_f32_fwd_cap<PK1, 10>, 5, 4, true},
@@ -729,7 +739,7 @@ int main(int argc, char** argv) {
     const bool want_rt = std::any_of(vars.begin(), vars.end(), [](const Variant& v) { return v.group == "rtpk"; });
     const bool want_coef = std::any_of(vars.begin(), vars.end(), [](const Variant& v) {
         return v.group == "rtpk" || v.group == "rtocc" || v.group == "invocc" || v.group == "invb" ||
-               v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc" ||
+               v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap" || v.group == "duocap16" || v.group == "jqrt" || v.group == "jqrtb" || v.group == "invc" ||
                v.group == "rtring";
     });
     if (want_coef) {
@@ -738,7 +748,7 @@ int main(int argc, char** argv) {
         for (auto& p : g_coef) CK(hipMalloc(&p, px * 4));
         if (std::any_of(vars.begin(), vars.end(),
                         [](const Variant& v) {
-                            return v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap";
+                            return v.group == "dropin" || v.group == "dropcap" || v.group == "fwdcap" || v.group == "duocap16";
                         })) {
             g_shift.resize(nsets);
             for (auto& p : g_shift) CK(hipMalloc(&p, px * 4));
